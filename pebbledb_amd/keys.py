@@ -1,0 +1,125 @@
+"""Key streams and the packed key layout handed across the C-ABI.
+
+The reference hashes ``key.encode("utf-8")`` (src/bloom_filter.py:43).  Across the boundary a
+batch of keys is either
+
+* fixed-width: ``n`` keys of ``key_len`` bytes, back to back (``uint8[n * key_len]``), or
+* variable-length: concatenated UTF-8 bytes plus ``uint64 offsets[n + 1]`` (key ``i`` is
+  ``bytes[offsets[i]:offsets[i+1]]``).
+
+Synthetic workloads — the same definitions are implemented by the device
+generators in csrc/keygen.hip and checked against these in tests:
+
+* ``splitmix_hex``: key ``i`` = 16 lowercase hex chars of ``splitmix64(seed + i)``.
+* ``varlen``: ``h = splitmix64((seed << 32) + i)``; length ``8 + h % 57`` (8..64 bytes);
+  char ``p`` = ``ALPHABET[byte(p % 8) of splitmix64(h + 1 + p // 8) % 36]``, alphabet [0-9a-z].
+"""
+from __future__ import annotations
+
+import numpy as np
+
+MASK64 = (1 << 64) - 1
+GOLDEN = 0x9E3779B97F4A7C15
+ALPHABET = b"0123456789abcdefghijklmnopqrstuvwxyz"
+HEX = b"0123456789abcdef"
+
+
+def splitmix64(x: int) -> int:
+    z = (x + GOLDEN) & MASK64
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & MASK64
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & MASK64
+    return z ^ (z >> 31)
+
+
+def _splitmix64_np(x: np.ndarray) -> np.ndarray:
+    z = x.astype(np.uint64) + np.uint64(GOLDEN)
+    z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return z ^ (z >> np.uint64(31))
+
+
+def splitmix_hex_keys_str(seed: int, start: int, n: int) -> list[str]:
+    return [format(splitmix64(seed + i), "016x") for i in range(start, start + n)]
+
+
+def splitmix_hex_keys(seed: int, start: int, n: int) -> np.ndarray:
+    """uint8[n, 16]: the fixed-width packed form of ``splitmix_hex_keys_str``."""
+    with np.errstate(over="ignore"):
+        idx = np.arange(start, start + n, dtype=np.uint64) + np.uint64(seed)
+        z = _splitmix64_np(idx)
+    shifts = np.arange(60, -4, -4, dtype=np.uint64)  # most significant nibble first
+    nib = ((z[:, None] >> shifts[None, :]) & np.uint64(0xF)).astype(np.uint8)
+    return np.frombuffer(HEX, dtype=np.uint8)[nib]
+
+
+def _varlen_one(seed: int, i: int) -> str:
+    h = splitmix64(((seed << 32) + i) & MASK64)
+    L = 8 + h % 57
+    out = bytearray(L)
+    for p in range(L):
+        w = splitmix64((h + 1 + p // 8) & MASK64)
+        out[p] = ALPHABET[((w >> (8 * (p % 8))) & 0xFF) % 36]
+    return out.decode("ascii")
+
+
+def varlen_keys_str(seed: int, start: int, n: int) -> list[str]:
+    return [_varlen_one(seed, i) for i in range(start, start + n)]
+
+
+def varlen_keys(seed: int, start: int, n: int) -> tuple[np.ndarray, np.ndarray]:
+    """(uint8 bytes, uint64 offsets[n+1]) packed form of ``varlen_keys_str``."""
+    with np.errstate(over="ignore"):
+        i = np.arange(start, start + n, dtype=np.uint64)
+        h = _splitmix64_np((np.uint64(seed) << np.uint64(32)) + i)
+        lens = (np.uint64(8) + h % np.uint64(57)).astype(np.int64)
+        words = np.empty((n, 8), dtype=np.uint64)
+        for j in range(8):
+            words[:, j] = _splitmix64_np(h + np.uint64(1 + j))
+    raw = words.view(np.uint8).reshape(n, 64)  # little-endian: byte p%8 of word p//8
+    chars = np.frombuffer(ALPHABET, dtype=np.uint8)[raw % 36]
+    mask = np.arange(64)[None, :] < lens[:, None]
+    data = chars[mask]
+    offsets = np.zeros(n + 1, dtype=np.uint64)
+    np.cumsum(lens, out=offsets[1:])
+    return np.ascontiguousarray(data), offsets
+
+
+class PackedKeys:
+    """A batch of keys in the boundary layout. ``key_len`` > 0 ⇒ fixed-width, offsets None."""
+
+    __slots__ = ("data", "offsets", "n", "key_len")
+
+    def __init__(self, data: np.ndarray, n: int, key_len: int = 0, offsets: np.ndarray | None = None):
+        self.data = np.ascontiguousarray(data, dtype=np.uint8).reshape(-1)
+        self.n = int(n)
+        self.key_len = int(key_len)
+        self.offsets = None if offsets is None else np.ascontiguousarray(offsets, dtype=np.uint64)
+        if self.key_len <= 0 and self.offsets is None:
+            raise ValueError("variable-length keys need offsets[n+1]")
+        if self.offsets is not None and len(self.offsets) != self.n + 1:
+            raise ValueError("offsets must have n+1 entries")
+
+    @classmethod
+    def from_strs(cls, keys) -> "PackedKeys":
+        enc = [k.encode("utf-8") for k in keys]  # bloom_filter.py:43
+        n = len(enc)
+        if n == 0:
+            return cls(np.zeros(0, np.uint8), 0, key_len=0, offsets=np.zeros(1, np.uint64))
+        lens = np.fromiter(map(len, enc), dtype=np.int64, count=n)
+        data = np.frombuffer(b"".join(enc), dtype=np.uint8)
+        L0 = int(lens[0])
+        if L0 > 0 and bool((lens == L0).all()):
+            return cls(data, n, key_len=L0)
+        offsets = np.zeros(n + 1, dtype=np.uint64)
+        np.cumsum(lens, out=offsets[1:])
+        return cls(data, n, key_len=0, offsets=offsets)
+
+    @classmethod
+    def fixed(cls, arr2d: np.ndarray) -> "PackedKeys":
+        a = np.ascontiguousarray(arr2d, dtype=np.uint8)
+        return cls(a.reshape(-1), a.shape[0], key_len=a.shape[1])
+
+    def key(self, i: int) -> bytes:
+        if self.key_len > 0:
+            return self.data[i * self.key_len:(i + 1) * self.key_len].tobytes()
+        return self.data[int(self.offsets[i]):int(self.offsets[i + 1])].tobytes()

@@ -1,0 +1,158 @@
+"""The oracle (oracle/) against every golden vector generated from the real reference.
+
+Fixtures come from tools/gen_golden.py, which imported the reference's own
+src/bloom_filter.py.  These tests need no GPU.
+"""
+import hashlib
+
+import numpy as np
+import pytest
+
+from conftest import load_golden
+from oracle.oracle import BigIntBloomPort, murmur3_x86_32, sizing
+from pebbledb_amd.keys import PackedKeys, splitmix_hex_keys, varlen_keys
+
+
+def test_mmh3_documented_values(oracle):
+    g = load_golden("mmh3_documented.json")
+    for c in g["cases"]:
+        h = oracle.murmur3(c["key"].encode(), c["seed"])
+        if "signed" in c:
+            assert h == c["signed"]
+            assert murmur3_x86_32(c["key"].encode(), c["seed"]) == c["signed"]
+        else:
+            assert h & 0xFFFFFFFF == c["unsigned"]
+
+
+def test_mmh3_vectors_all_tail_lengths_and_seeds(oracle):
+    for c in load_golden("mmh3_vectors.json")["cases"]:
+        key = bytes.fromhex(c["key_hex"])
+        if "h" in c:
+            assert [oracle.murmur3(key, s) for s in range(16)] == c["h"]
+            assert [murmur3_x86_32(key, s) for s in range(16)] == c["h"]
+        else:
+            assert oracle.murmur3(key, c["seed"]) == c["h1"]
+
+
+def test_index_math_floor_mod(oracle):
+    for c in load_golden("index_math.json")["cases"]:
+        m = 8 * c["nb_bytes"]
+        for key, want in zip(c["keys"], c["indices"]):
+            assert oracle.indices(key.encode("utf-8"), c["k"], m) == want, (c["nb_bytes"], key)
+
+
+def test_reference_kats(oracle):
+    for c in load_golden("reference_kats.json")["cases"]:
+        pk = PackedKeys.from_strs(c["keys"])
+        bm = oracle.build(c["nb_bytes"], c["k"], pk)
+        assert bm.tobytes() + bytes([c["k"]]) == bytes.fromhex(c["to_bytes_hex"])
+        assert int.from_bytes(bm.tobytes(), "little") == int(c["bits"])
+        hm = oracle.probe(bm, c["k"], PackedKeys.from_strs(c["probes"]))
+        got = [bool(hm[i >> 3] >> (i & 7) & 1) for i in range(len(c["probes"]))]
+        assert got == c["probe_results"]
+
+
+def test_reference_test_file_bytes(oracle):
+    # test_bloom_filter.py:43-45 and :59-61, verbatim expected values
+    bm = oracle.build(1, 2, PackedKeys.from_strs(["key1", "key2", "key3"]))
+    assert bm.tobytes() + b"\x02" == b"3" + b"\x02"
+    bm = oracle.build(3, 2, PackedKeys.from_strs(["key1", "key2", "key3"]))
+    assert bm.tobytes() + b"\x02" == b"\x003\x10" + b"\x02"
+
+
+def test_sizing_matches_reference():
+    for c in load_golden("sizing.json")["cases"]:
+        assert sizing(c["n"], c["p"]) == (c["nb_bytes"], c["k"])
+
+
+def _check_desc(bm: np.ndarray, d):
+    b = bm.tobytes()
+    assert len(b) == d["nb_bytes"]
+    assert hashlib.sha256(b).hexdigest() == d["sha256"]
+    assert int(np.unpackbits(bm).sum()) == d["popcount"]
+    if "to_bytes_hex" in d:
+        assert b + bytes([d["nb_hash_functions"]]) == bytes.fromhex(d["to_bytes_hex"])
+
+
+def test_config1(oracle):
+    g = load_golden("config1.json")
+    keys = [f"{i:016d}" for i in range(1000)]
+    d = g["config1"]
+    bm = oracle.build(1024, 4, PackedKeys.from_strs(keys))
+    _check_desc(bm, d)
+    hm = oracle.probe(bm, 4, PackedKeys.from_strs([f"{i:016d}" for i in range(11000)]))
+    assert hm.tobytes().hex() == d["probe_hitmask_hex"]
+    p = g["product_p0001"]
+    nb, k = sizing(1000, 0.001)
+    assert (nb, k) == (p["nb_bytes"], p["nb_hash_functions"])
+    _check_desc(oracle.build(nb, k, PackedKeys.from_strs(keys)), p)
+
+
+def test_splitmix16(oracle):
+    g = load_golden("splitmix16.json")
+    members = PackedKeys.fixed(splitmix_hex_keys(g["seed"], 0, g["members"]))
+    non = PackedKeys.fixed(splitmix_hex_keys(g["seed"], g["nonmember_start"], g["nonmembers"]))
+    assert [members.key(i).decode() for i in range(4)] == g["pow2"]["keys_first"]
+    bm = oracle.build(8192, 6, members)
+    _check_desc(bm, g["pow2"])
+    assert oracle.probe(bm, 6, non).tobytes().hex() == g["pow2"]["hitmask_nonmembers_hex"]
+    first = PackedKeys.fixed(splitmix_hex_keys(g["seed"], 0, 2048))
+    assert oracle.probe(bm, 6, first).tobytes().hex() == g["pow2"]["hitmask_members_first2048_hex"]
+    m5 = PackedKeys.fixed(splitmix_hex_keys(g["seed"], 0, 5000))
+    bm2 = oracle.build(6007, 7, m5)
+    _check_desc(bm2, g["odd"])
+    assert oracle.probe(bm2, 7, non).tobytes().hex() == g["odd"]["hitmask_nonmembers_hex"]
+
+
+def test_varlen(oracle):
+    g = load_golden("varlen.json")
+    data, off = varlen_keys(g["seed"], 0, g["members"])
+    pk = PackedKeys(data, g["members"], offsets=off)
+    assert [pk.key(i).decode() for i in range(3)] == g["varlen"]["keys_first"]
+    bm = oracle.build(8192, 8, pk)
+    _check_desc(bm, g["varlen"])
+    d2, o2 = varlen_keys(g["seed"], g["nonmember_start"], g["nonmembers"])
+    hm = oracle.probe(bm, 8, PackedKeys(d2, g["nonmembers"], offsets=o2))
+    assert hm.tobytes().hex() == g["varlen"]["hitmask_nonmembers_hex"]
+    sk = [(f"{i:08d}" * 8)[:8 + i % 57] for i in range(1000)]
+    _check_desc(oracle.build(1024, 8, PackedKeys.from_strs(sk)), g["survey_family"])
+
+
+def test_unicode(oracle):
+    g = load_golden("unicode.json")
+    bm = oracle.build(g["nb_bytes"], g["nb_hash_functions"], PackedKeys.from_strs(g["keys"]))
+    _check_desc(bm, g)
+    probes = g["keys"] + [f"absent-{i}" for i in range(200)]
+    hm = oracle.probe(bm, g["nb_hash_functions"], PackedKeys.from_strs(probes))
+    assert hm.tobytes().hex() == g["hitmask_hex"]
+
+
+def test_large_m_indices(oracle):
+    for c in load_golden("large_m.json")["cases"]:
+        m = 8 * c["nb_bytes"]
+        got = sorted({i for j in range(64) for i in oracle.indices(f"{j:016d}".encode(), c["k"], m)})
+        assert got == c["set_bits"]
+        if m >= 2 ** 31:  # only [0, 2^31) U [m - 2^31, m) is reachable
+            assert all(b < 2 ** 31 or b >= m - 2 ** 31 for b in got)
+
+
+@pytest.mark.parametrize("nb,k", [(64, 3), (1024, 4), (999, 5)])
+def test_bigint_port_equals_c_oracle(oracle, nb, k):
+    keys = [f"key-{i}" for i in range(300)]
+    port = BigIntBloomPort(nb, k)
+    for key in keys:
+        port.add(key)
+    bm = oracle.build(nb, k, PackedKeys.from_strs(keys))
+    assert port.to_bytes() == bm.tobytes() + bytes([k])
+    probes = keys + [f"nokey-{i}" for i in range(300)]
+    hm = oracle.probe(bm, k, PackedKeys.from_strs(probes))
+    assert [port.may_contain(p) for p in probes] == [bool(hm[i >> 3] >> (i & 7) & 1) for i in range(600)]
+
+
+def test_omp_twins_equal_serial(oracle):
+    pk = PackedKeys.fixed(splitmix_hex_keys(7, 0, 50000))
+    a = oracle.build(40000, 6, pk)
+    b = oracle.build(40000, 6, pk, omp=True)
+    assert (a == b).all()
+    q = PackedKeys.fixed(splitmix_hex_keys(7, 25000, 50001))
+    assert (oracle.probe(a, 6, q) == oracle.probe(a, 6, q, omp=True)).all()
