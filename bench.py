@@ -1,0 +1,265 @@
+"""Benchmark: device-resident bloom build + probe (BASELINE.json metric), one process per GPU.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c1|c3] [--no-cpu-baseline]
+
+Config c2 (default, BASELINE.json configs[1]): per GPU one SSTable filter of m = 2^30 bits
+(nb_bytes = 128 MiB), k = 6, built from 10M 16-byte keys, then probed with 20M keys (the 10M
+members + 10M non-members).  A step = clear + build (10M keys) + probe (20M keys), all on the
+filter's HIP stream, keys already resident in HBM.  Ranks hold independent filters over
+disjoint key ranges (weak scaling, no collective on the data path: SURVEY.md §8e).
+
+value = (build keys + probe keys) summed over ranks / max-over-ranks wall time, in Mkeys/s.
+Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
+
+CONFIGS = {
+    # name: (n_build, nb_bytes, k, key kind)
+    "c1": (1000, 1024, 4, "hex16"),
+    "c2": (10_000_000, 2 ** 27, 6, "hex16"),
+    "c3": (100_000_000, 2 ** 30, 8, "varlen"),
+}
+SEED = 0x5EEDB100
+SEED_VAR = 0xC3
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--build-mode", type=int, default=0, help="0 auto, 1 atomic, 2 tiled")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the bounded CPU sample")
+    return ap.parse_args()
+
+
+def algorithmic_bytes(n, L, k, m_bits, offsets):
+    """build = n·L + 8·n·k + m/8 (+8n offsets); probe = n·L + 4·n·k + n/8."""
+    build = n * L + 8 * n * k + m_bits // 8 + (8 * n if offsets else 0)
+    return build
+
+
+def probe_bytes(n, L, k, offsets):
+    return n * L + 4 * n * k + n // 8 + (8 * n if offsets else 0)
+
+
+def cpu_baseline(nb_bytes, k, kind, budget_s):
+    """The reference algorithm as the reference runs it (oracle/oracle.py BigIntBloomPort: one
+    Python big-int bitmap, `bits |= 1 << idx` per hashed bit) on the SAME filter size, timed on
+    a bounded sample of the workload's keys; plus the C oracle on all host cores."""
+    import numpy as np
+
+    from oracle.oracle import BigIntBloomPort, COracle
+    from pebbledb_amd.keys import PackedKeys, splitmix_hex_keys, splitmix_hex_keys_str, varlen_keys_str
+
+    strs = (splitmix_hex_keys_str(SEED, 0, 64) if kind == "hex16" else varlen_keys_str(SEED_VAR, 0, 64))
+    port = BigIntBloomPort(nb_bytes, k)
+    t0 = time.perf_counter()
+    nb = 0
+    while nb < len(strs) and time.perf_counter() - t0 < budget_s / 2:
+        port.add(strs[nb])
+        nb += 1
+    t_build = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    npb = 0
+    while npb < len(strs) and time.perf_counter() - t0 < budget_s / 2:
+        port.may_contain(strs[npb] if npb % 2 == 0 else strs[npb] + "x")
+        npb += 1
+    t_probe = time.perf_counter() - t0
+    # the workload's mix is 1 build key : 2 probe keys → keys/s = 3 / (t_add + 2·t_probe)
+    tb, tp = t_build / max(nb, 1), t_probe / max(npb, 1)
+    rate = 3.0 / (tb + 2.0 * tp) if nb and npb else 0.0
+    # fair native number: the C oracle with OpenMP on every host core, 2M keys
+    o = COracle()
+    n_c = 2_000_000
+    pk = PackedKeys.fixed(splitmix_hex_keys(SEED, 0, n_c))
+    q = PackedKeys.fixed(splitmix_hex_keys(SEED, 0, 2 * n_c))
+    t0 = time.perf_counter()
+    bm = o.build(nb_bytes, k, pk, omp=True)
+    o.probe(bm, k, q, omp=True)
+    t_c = time.perf_counter() - t0
+    return {
+        "value": rate / 1e6,
+        "unit": "Mkeys/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": (f"reference algorithm (Python big-int bitmap, oracle/oracle.py BigIntBloomPort) on the "
+                   f"full-size filter nb_bytes={nb_bytes}, k={k}: {nb} build keys in {t_build:.2f}s + {npb} probes "
+                   f"in {t_probe:.2f}s; rate = 3/(t_add + 2*t_probe), the step's 1:2 build:probe mix"),
+        "build_s_per_key": t_build / max(nb, 1),
+        "probe_s_per_key": t_probe / max(npb, 1),
+        "c_oracle_omp": {"value": 3 * n_c / t_c / 1e6, "unit": "Mkeys/s", "cores": o.num_threads(),
+                         "sample": f"{n_c} builds + {2 * n_c} probes, same filter size"},
+    }
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"warning: WORLD_SIZE={world} but --gpus={args.gpus}", file=sys.stderr)
+
+    import torch
+    import torch.distributed as dist
+    import numpy as np
+
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group(backend="nccl", init_method="env://", device_id=torch.device("cuda", local))
+
+    from pebbledb_amd import BloomFilter, _native
+    from pebbledb_amd.bloom_filter import set_default_device
+
+    set_default_device(local)
+    n, nb_bytes, k, kind = CONFIGS[args.config]
+    m_bits = 8 * nb_bytes
+    # this rank's SSTable: keys [rank*2n, rank*2n + n) are members, [.. + n, .. + 2n) are absent
+    start = rank * 2 * n
+    L = _native.lib()
+    if kind == "hex16":
+        keys = torch.empty(2 * n * 16, dtype=torch.uint8, device="cuda")
+        _native.check(L.pbf_gen_splitmix_hex(local, None, keys.data_ptr(), SEED, start, 2 * n), "gen")
+        offs = None
+        key_bytes = 16.0
+    else:
+        from pebbledb_amd.keys import _splitmix64_np
+        idx = np.arange(start, start + 2 * n, dtype=np.uint64)
+        with np.errstate(over="ignore"):
+            h = _splitmix64_np((np.uint64(SEED_VAR) << np.uint64(32)) + idx)
+        lens = (8 + h % np.uint64(57)).astype(np.int64)
+        o = np.zeros(2 * n + 1, dtype=np.int64)
+        np.cumsum(lens, out=o[1:])
+        offs = torch.from_numpy(o).cuda()
+        keys = torch.empty(int(o[-1]), dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()
+        _native.check(L.pbf_gen_varlen(local, None, keys.data_ptr(), offs.data_ptr(), SEED_VAR, start, 2 * n), "gen")
+        key_bytes = float(o[n]) / n
+        del h, lens, idx
+    hitmask = torch.zeros((2 * n + 7) // 8, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+
+    bf = BloomFilter(nb_bytes, k, device=local)
+    if args.build_mode:
+        bf.set_build_mode(args.build_mode)
+    stream = torch.cuda.ExternalStream(bf.stream)
+
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record(stream)
+        bf.clear()  # the build's time includes zeroing the bitmap (a memset, or the tile pass)
+        if offs is None:
+            bf.add_device_fixed(keys.data_ptr(), 16, n)
+        else:
+            bf.add_device(keys.data_ptr(), offs.data_ptr(), n)
+        if ev is not None:
+            ev[1].record(stream)
+        if offs is None:
+            bf.probe_device_fixed(keys.data_ptr(), 16, 2 * n, hitmask.data_ptr())
+        else:
+            bf.probe_device(keys.data_ptr(), offs.data_ptr(), 2 * n, hitmask.data_ptr())
+        if ev is not None:
+            ev[2].record(stream)
+
+    for _ in range(args.warmup):
+        step()
+    bf.sync()
+    # correctness guard on the measured data: every member must hit
+    hm = hitmask.cpu().numpy()
+    members_ok = bool((np.unpackbits(hm, bitorder="little")[:n] == 1).all())
+    fp = int(np.unpackbits(hm, bitorder="little")[n:2 * n].sum())
+
+    events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    bf.sync()
+    t0 = time.perf_counter()
+    for s in range(args.steps):
+        step(events[s])
+    bf.sync()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    elapsed = t1 - t0
+    build_ms = sum(e[0].elapsed_time(e[1]) for e in events) / args.steps
+    probe_ms = sum(e[1].elapsed_time(e[2]) for e in events) / args.steps
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        ok = torch.tensor([1 if members_ok else 0], dtype=torch.int32, device="cuda")
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        members_ok = bool(ok.item())
+
+    if rank == 0:
+        ms_per_step = elapsed / args.steps * 1e3
+        keys_per_step = 3 * n * world
+        value = keys_per_step * args.steps / elapsed / 1e6
+        offsets = offs is not None
+        b_build = algorithmic_bytes(n, key_bytes, k, m_bits, offsets)
+        b_probe = probe_bytes(2 * n, key_bytes, k, offsets)
+        ach_build = b_build / (build_ms * 1e-3) / 1e9
+        ach_probe = b_probe / (probe_ms * 1e-3) / 1e9
+        if build_ms >= probe_ms:
+            dom = {"kernel": f"build pass ({'tiled' if bf.last_build_mode == 2 else 'atomic'}: "
+                             f"{'k_hist+k_colscan+k_basescan+k_scatter+k_tile' if bf.last_build_mode == 2 else 'k_build_atomic'})",
+                   "achieved": ach_build, "ms": build_ms, "bytes": b_build}
+        else:
+            dom = {"kernel": "k_probe", "achieved": ach_probe, "ms": probe_ms, "bytes": b_probe}
+        out = {
+            "metric": "Mkeys/s bloom build+probe (device-resident), 10M 16B keys; 1/2/4/8 GPU",
+            "value": round(value, 3),
+            "unit": "Mkeys/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic (splitmix64 hex keys generated on device)",
+            "config": {"workload": f"{args.config}: build {n} keys of {key_bytes:.1f} B into m=2^{m_bits.bit_length() - 1}"
+                                   f" bits (nb_bytes={nb_bytes}), k={k}; probe {2 * n} keys ({n} members + {n} absent)"
+                                   f"; one filter per GPU", "n_build": n, "n_probe": 2 * n, "nb_bytes": nb_bytes, "k": k,
+                       "keys_per_step_per_gpu": 3 * n, "parallelism": f"filter-per-gpu x{world}"},
+            "build_ms": round(build_ms, 4),
+            "probe_ms": round(probe_ms, 4),
+            "build_Mkeys_s_per_gpu": round(n / build_ms / 1e3, 1),
+            "probe_Mkeys_s_per_gpu": round(2 * n / probe_ms / 1e3, 1),
+            "build_mode": bf.last_build_mode,
+            "roofline": {"bound": "hbm", "achieved": round(dom["achieved"], 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(dom["achieved"] / HBM_PEAK_GBS, 4), "traffic": None, "kernel": dom["kernel"],
+                         "algorithmic_bytes": int(dom["bytes"]), "avg_ms": round(dom["ms"], 4)},
+            "roofline_build": {"achieved": round(ach_build, 1), "frac": round(ach_build / HBM_PEAK_GBS, 4),
+                               "algorithmic_bytes": int(b_build)},
+            "roofline_probe": {"achieved": round(ach_probe, 1), "frac": round(ach_probe / HBM_PEAK_GBS, 4),
+                               "algorithmic_bytes": int(b_probe)},
+            "check": {"members_all_hit": members_ok, "false_positives": fp, "probes_absent": n},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(nb_bytes, k, kind, args.cpu_seconds)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    del bf
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,120 @@
+/*
+ * pebblebloom — C-ABI of the MI355X bloom-filter engine (libpebblebloom.so).
+ *
+ * Drop-in boundary for MaudGautier/pebbledb's per-SSTable filter, src/bloom_filter.py.  The
+ * reference has no FFI layer: its boundary is the Python class BloomFilter, whose callers are
+ * src/sstable.py:274 (build), :82 (to_bytes), :100 (from_bytes), :146 (__eq__) and
+ * src/lsm_storage.py:165,175 (may_contain).  pebbledb_amd/bloom_filter.py keeps that class's
+ * surface and binds every entry point below through ctypes.
+ *
+ * Conventions
+ *   - All functions return 0 (PBF_OK) or a negative PBF_ERR_*; pbf_last_error() gives the
+ *     message of the last failure on the calling thread.
+ *   - Keys are UTF-8 bytes (bloom_filter.py:43).  A batch is either fixed-width (key i =
+ *     keys[i*key_len, (i+1)*key_len)) or variable-length (key i = keys[offsets[i] - offsets[0],
+ *     offsets[i+1] - offsets[0]); offsets has n+1 entries).
+ *   - keys_on_device = 0: keys/offsets/hitmask are host pointers; the call copies what it needs
+ *     (pinned staging + hipMemcpyAsync) and returns when the host buffers may be reused.
+ *     keys_on_device = 1: they are device pointers on the filter's device; the call is
+ *     asynchronous on the filter's stream (pbf_stream) and the caller keeps them alive until
+ *     pbf_sync (or an event recorded on that stream) completes.
+ *   - A handle is one filter on one device with one HIP stream.  Calls on one handle are
+ *     serialised by the caller; distinct handles may be driven from distinct host threads
+ *     (the reference builds a filter under the flush mutex, lsm_storage.py:220, and only
+ *     reads it afterwards, lsm_storage.py:164-179).
+ */
+#ifndef PEBBLEBLOOM_H
+#define PEBBLEBLOOM_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PBF_OK 0
+#define PBF_ERR_INVALID (-1)   /* bad argument (null handle or pointer, size mismatch) */
+#define PBF_ERR_HIP (-2)       /* a HIP runtime call failed */
+#define PBF_ERR_ZERO_SIZE (-3) /* nb_bytes == 0: the reference raises ZeroDivisionError at
+                                  `hashed_key % self.bits_size` (bloom_filter.py:47) */
+
+/* Build strategies (pbf_set_build_mode).  All give bit-identical bitmaps. */
+#define PBF_BUILD_AUTO 0
+#define PBF_BUILD_ATOMIC 1 /* one lane per key, k global atomicOr */
+#define PBF_BUILD_TILED 2  /* partition positions by LDS tile, OR in LDS, write tiles once */
+
+typedef struct pbf_filter pbf_filter_t;
+
+/* Library version (major*10000 + minor*100 + patch). */
+int pbf_version(void);
+
+/* Number of visible HIP devices. */
+int pbf_device_count(int* count);
+
+/* BloomFilter(nb_bytes, nb_hash_functions) — bloom_filter.py:26-31.  The bitmap is
+ * 8*nb_bytes bits, all zero.  nb_bytes == 0 → PBF_ERR_ZERO_SIZE (the Python layer keeps such a
+ * filter host-side and raises ZeroDivisionError on add/may_contain, like the reference).
+ * Any nb_hash_functions is accepted, as in the reference; serialising one above 255 fails in
+ * the Python layer exactly where the reference's struct.pack("B", k) does (bloom_filter.py:80). */
+int pbf_create(int device, uint64_t nb_bytes, uint32_t nb_hash_functions, pbf_filter_t** out);
+int pbf_destroy(pbf_filter_t* f);
+
+/* Reset to the all-zero filter (bits = 0, bloom_filter.py:31). */
+int pbf_clear(pbf_filter_t* f);
+
+/* BloomFilter.add for a batch of keys (bloom_filter.py:60-65): ORs k bits per key. */
+int pbf_add_fixed(pbf_filter_t* f, const uint8_t* keys, uint32_t key_len, uint64_t n, int keys_on_device);
+int pbf_add(pbf_filter_t* f, const uint8_t* keys, const uint64_t* offsets, uint64_t n, int keys_on_device);
+
+/* BloomFilter.may_contain for a batch (bloom_filter.py:67-74).  hitmask receives ceil(n/8)
+ * bytes, LSB-first: bit (i & 7) of hitmask[i >> 3] = may_contain(key i).  The hitmask pointer
+ * is host or device memory as keys_on_device says. */
+int pbf_probe_fixed(pbf_filter_t* f, const uint8_t* keys, uint32_t key_len, uint64_t n, uint8_t* hitmask,
+                    int keys_on_device);
+int pbf_probe(pbf_filter_t* f, const uint8_t* keys, const uint64_t* offsets, uint64_t n, uint8_t* hitmask,
+              int keys_on_device);
+
+/* The k bit indices of each key, BloomFilter._hash (bloom_filter.py:38-49): out[i*k + s] =
+ * mmh3.hash(key_i, s) % bits_size (Python floor-mod).  out is host or device memory as
+ * keys_on_device says (n*k uint64).  Used for index-math parity at any m. */
+int pbf_hash_indices_fixed(pbf_filter_t* f, const uint8_t* keys, uint32_t key_len, uint64_t n, uint64_t* out,
+                           int keys_on_device);
+int pbf_hash_indices(pbf_filter_t* f, const uint8_t* keys, const uint64_t* offsets, uint64_t n, uint64_t* out,
+                     int keys_on_device);
+
+/* to_bytes() minus the trailing k byte (bloom_filter.py:76-81): copies the nb_bytes-byte
+ * little-endian bitmap into host memory `out` (nb_bytes must equal the filter's). */
+int pbf_get_bitmap(pbf_filter_t* f, uint8_t* out, uint64_t nb_bytes);
+
+/* from_bytes() (bloom_filter.py:83-90): loads an nb_bytes-byte bitmap from host memory. */
+int pbf_set_bitmap(pbf_filter_t* f, const uint8_t* in, uint64_t nb_bytes);
+
+/* Population count of the bitmap (device reduction; host-visible result). */
+int pbf_popcount(pbf_filter_t* f, uint64_t* out);
+
+/* Wait for all work queued on the filter's stream. */
+int pbf_sync(pbf_filter_t* f);
+
+/* The filter's hipStream_t (for events / interop) and its device bitmap (uint32 words). */
+void* pbf_stream(pbf_filter_t* f);
+void* pbf_device_bitmap(pbf_filter_t* f);
+
+/* Select the build strategy (PBF_BUILD_*); the strategy actually used by the last add is
+ * returned by pbf_last_build_mode. */
+int pbf_set_build_mode(pbf_filter_t* f, int mode);
+int pbf_last_build_mode(pbf_filter_t* f);
+
+/* Synthetic keys straight into device memory (bench / tests; definitions in
+ * pebbledb_amd/keys.py): 16 hex chars of splitmix64(seed + start + i), and the variable-length
+ * 8..64-byte family (offsets must already hold the n+1 offsets, relative to offsets[0]). */
+int pbf_gen_splitmix_hex(int device, void* stream, uint8_t* out_dev, uint64_t seed, uint64_t start, uint64_t n);
+int pbf_gen_varlen(int device, void* stream, uint8_t* out_dev, const uint64_t* offsets_dev, uint64_t seed,
+                   uint64_t start, uint64_t n);
+
+/* Message of the last failure on this thread ("" if none). */
+const char* pbf_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PEBBLEBLOOM_H */

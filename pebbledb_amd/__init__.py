@@ -1,0 +1,9 @@
+"""pebbledb_amd — MI355X-native bloom-filter engine for pebbledb's per-SSTable filter path.
+
+Drop-in for MaudGautier/pebbledb ``src/bloom_filter.py`` (``BloomFilter``), backed by
+hand-written HIP kernels for gfx950 in ``libpebblebloom.so`` (C-ABI: include/pebblebloom.h).
+"""
+from .bloom_filter import BloomFilter, set_default_device
+from .keys import PackedKeys
+
+__all__ = ["BloomFilter", "PackedKeys", "set_default_device"]

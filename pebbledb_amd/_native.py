@@ -1,0 +1,98 @@
+"""ctypes binding of libpebblebloom.so (include/pebblebloom.h).
+
+There is no fallback: if the library is missing or fails to load, every product call raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libpebblebloom.so")
+HEADER = os.path.join(os.path.dirname(_HERE), "include", "pebblebloom.h")
+
+PBF_OK = 0
+PBF_ERR_INVALID = -1
+PBF_ERR_HIP = -2
+PBF_ERR_ZERO_SIZE = -3
+PBF_BUILD_AUTO, PBF_BUILD_ATOMIC, PBF_BUILD_TILED = 0, 1, 2
+
+_u8p = ctypes.c_void_p
+_vp = ctypes.c_void_p
+_u64 = ctypes.c_uint64
+_u32 = ctypes.c_uint32
+_int = ctypes.c_int
+
+# name → (restype, argtypes); must cover every function declared in include/pebblebloom.h
+SIGNATURES = {
+    "pbf_version": (_int, []),
+    "pbf_device_count": (_int, [ctypes.POINTER(_int)]),
+    "pbf_create": (_int, [_int, _u64, _u32, ctypes.POINTER(_vp)]),
+    "pbf_destroy": (_int, [_vp]),
+    "pbf_clear": (_int, [_vp]),
+    "pbf_add_fixed": (_int, [_vp, _u8p, _u32, _u64, _int]),
+    "pbf_add": (_int, [_vp, _u8p, _vp, _u64, _int]),
+    "pbf_probe_fixed": (_int, [_vp, _u8p, _u32, _u64, _u8p, _int]),
+    "pbf_probe": (_int, [_vp, _u8p, _vp, _u64, _u8p, _int]),
+    "pbf_hash_indices_fixed": (_int, [_vp, _u8p, _u32, _u64, _vp, _int]),
+    "pbf_hash_indices": (_int, [_vp, _u8p, _vp, _u64, _vp, _int]),
+    "pbf_get_bitmap": (_int, [_vp, _u8p, _u64]),
+    "pbf_set_bitmap": (_int, [_vp, _u8p, _u64]),
+    "pbf_popcount": (_int, [_vp, ctypes.POINTER(_u64)]),
+    "pbf_sync": (_int, [_vp]),
+    "pbf_stream": (_vp, [_vp]),
+    "pbf_device_bitmap": (_vp, [_vp]),
+    "pbf_set_build_mode": (_int, [_vp, _int]),
+    "pbf_last_build_mode": (_int, [_vp]),
+    "pbf_gen_splitmix_hex": (_int, [_int, _vp, _u8p, _u64, _u64, _u64]),
+    "pbf_gen_varlen": (_int, [_int, _vp, _u8p, _vp, _u64, _u64, _u64]),
+    "pbf_last_error": (ctypes.c_char_p, []),
+}
+
+_lib = None
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def header_functions() -> list[str]:
+    """Every function name declared in include/pebblebloom.h."""
+    with open(HEADER) as f:
+        text = f.read()
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\**\s+\**(pbf_\w+)\s*\(", text, re.M)))
+
+
+def lib():
+    """Load libpebblebloom.so (built by pebbledb_amd/build.py); raise loudly if absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise NativeError(f"{LIB_PATH} is not built: run `python -c 'import __graft_entry__ as g; g.build()'` "
+                          "(there is no CPU fallback)")
+    L = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc == PBF_OK:
+        return
+    msg = lib().pbf_last_error().decode(errors="replace")
+    if rc == PBF_ERR_ZERO_SIZE:
+        raise ZeroDivisionError("integer modulo by zero")
+    if rc == PBF_ERR_INVALID:
+        raise ValueError(f"{what}: {msg}")
+    raise NativeError(f"{what}: HIP failure: {msg}")
+
+
+def device_count() -> int:
+    n = _int(0)
+    check(lib().pbf_device_count(ctypes.byref(n)), "pbf_device_count")
+    return n.value

@@ -1,0 +1,282 @@
+"""``BloomFilter`` — drop-in for MaudGautier/pebbledb ``src/bloom_filter.py`` on MI355X.
+
+Same constructor, attributes and methods as the reference class (bloom_filter.py:8-119):
+``BloomFilter(nb_bytes, nb_hash_functions, bits=None)``, ``add``, ``may_contain``,
+``to_bytes``, ``from_bytes``, ``build_from_keys_and_fp_rate``, ``__eq__`` and the attributes
+``nb_bytes``, ``bits_size``, ``nb_hash_functions``, ``bits``.  Results are bit-identical to the
+reference (tests/test_gpu_parity.py): MurmurHash3_x86_32 with seeds 0..k-1 over the key's
+UTF-8 bytes, Python floor-mod of the signed hash by ``bits_size``.
+
+The bitmap lives in HBM behind a ``pbf_filter_t`` handle (libpebblebloom.so, ctypes).  Per-key
+``add()`` calls are buffered on the host and sent as one batch at the next read (probe,
+serialisation, ``bits``), so an SSTableBuilder-style loop of ``add`` costs one kernel
+pipeline, not one launch per key.  Batch entry points ``add_many`` / ``may_contain_many`` take
+``list[str]`` or ``PackedKeys`` (host numpy) directly.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import struct
+from math import ceil, log
+from typing import Iterable, Optional
+
+import numpy as np
+
+from . import _native
+from .keys import PackedKeys
+
+_PENDING_FLUSH = 1 << 16
+_default_device = int(os.environ.get("PBF_DEVICE", os.environ.get("LOCAL_RANK", "0")))
+
+
+def set_default_device(device: int) -> None:
+    global _default_device
+    _default_device = int(device)
+
+
+def _vp(a: np.ndarray | None):
+    return None if a is None else ctypes.c_void_p(a.ctypes.data)
+
+
+class BloomFilter:
+    """See module docstring; reference: src/bloom_filter.py:8."""
+
+    def __init__(self, nb_bytes: int, nb_hash_functions: int, bits: Optional[int] = None,
+                 device: Optional[int] = None):
+        # bloom_filter.py:26-31
+        self.nb_bytes = nb_bytes
+        self.bits_size = 8 * nb_bytes
+        self.nb_hash_functions = nb_hash_functions
+        self.device = _default_device if device is None else int(device)
+        self._pending: list[str] = []
+        self._h = None
+        if nb_bytes > 0:
+            h = ctypes.c_void_p()
+            _native.check(_native.lib().pbf_create(self.device, nb_bytes, nb_hash_functions, ctypes.byref(h)),
+                          "pbf_create")
+            self._h = h
+        if bits:
+            self._upload_int(bits)
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and _native._lib is not None:
+            _native._lib.pbf_destroy(h)
+            self._h = None
+
+    # ------------------------------------------------------------------ helpers
+    def _require_modulus(self):
+        """The reference computes `hash % bits_size` per hash function (bloom_filter.py:47)."""
+        if self.nb_hash_functions <= 0:
+            return False
+        if self.nb_bytes == 0:
+            raise ZeroDivisionError("integer modulo by zero")
+        if self.nb_bytes < 0:
+            raise ValueError("negative shift count")
+        return True
+
+    def _upload_int(self, bits: int) -> None:
+        if self.nb_bytes <= 0:
+            raise ValueError("bits given for a filter with nb_bytes <= 0")
+        data = np.frombuffer(int(bits).to_bytes(self.nb_bytes, "little"), dtype=np.uint8)
+        _native.check(_native.lib().pbf_set_bitmap(self._h, _vp(data), self.nb_bytes), "pbf_set_bitmap")
+
+    def _flush(self) -> None:
+        if self._pending:
+            pend, self._pending = self._pending, []
+            self._add_packed(PackedKeys.from_strs(pend))
+
+    def _add_packed(self, pk: PackedKeys) -> None:
+        if pk.n == 0 or not self._require_modulus():
+            return
+        L = _native.lib()
+        if pk.key_len > 0:
+            rc = L.pbf_add_fixed(self._h, _vp(pk.data), pk.key_len, pk.n, 0)
+        else:
+            rc = L.pbf_add(self._h, _vp(pk.data), _vp(pk.offsets), pk.n, 0)
+        _native.check(rc, "pbf_add")
+
+    def _probe_packed(self, pk: PackedKeys) -> np.ndarray:
+        out = np.zeros((pk.n + 7) // 8, dtype=np.uint8)
+        if pk.n == 0:
+            return out
+        if not self._require_modulus():  # k == 0: the AND over no bits is True
+            out[:] = 0xFF
+            if pk.n % 8:
+                out[-1] = (1 << (pk.n % 8)) - 1
+            return out
+        self._flush()
+        L = _native.lib()
+        if pk.key_len > 0:
+            rc = L.pbf_probe_fixed(self._h, _vp(pk.data), pk.key_len, pk.n, _vp(out), 0)
+        else:
+            rc = L.pbf_probe(self._h, _vp(pk.data), _vp(pk.offsets), pk.n, _vp(out), 0)
+        _native.check(rc, "pbf_probe")
+        return out
+
+    def bitmap(self) -> bytes:
+        """The nb_bytes-long little-endian bitmap (to_bytes() without the k byte)."""
+        if self.nb_bytes <= 0:
+            return b""
+        self._flush()
+        out = np.empty(self.nb_bytes, dtype=np.uint8)
+        _native.check(_native.lib().pbf_get_bitmap(self._h, _vp(out), self.nb_bytes), "pbf_get_bitmap")
+        return out.tobytes()
+
+    # ------------------------------------------------------------------ reference surface
+    @property
+    def bits(self) -> int:
+        """The filter as one Python int (bloom_filter.py:31), materialised on demand."""
+        return int.from_bytes(self.bitmap(), "little")
+
+    @bits.setter
+    def bits(self, value: int) -> None:
+        self._pending = []
+        if self.nb_bytes > 0:
+            _native.check(_native.lib().pbf_clear(self._h), "pbf_clear")
+            if value:
+                self._upload_int(value)
+
+    def __eq__(self, other):
+        # bloom_filter.py:33-36 — compares bits and k only (not nb_bytes)
+        if not isinstance(other, BloomFilter):
+            return NotImplemented
+        if self.nb_hash_functions != other.nb_hash_functions:
+            return False
+        return self.bitmap().rstrip(b"\0") == other.bitmap().rstrip(b"\0")
+
+    __hash__ = None
+
+    def _hash(self, key: str) -> list[int]:
+        """bloom_filter.py:38-49 — the k bit indices of `key`, computed on the GPU."""
+        if not self._require_modulus():
+            return []
+        pk = PackedKeys.from_strs([key])
+        k = self.nb_hash_functions
+        out = np.zeros(k, dtype=np.uint64)
+        L = _native.lib()
+        if pk.key_len > 0:
+            rc = L.pbf_hash_indices_fixed(self._h, _vp(pk.data), pk.key_len, 1, _vp(out), 0)
+        else:
+            rc = L.pbf_hash_indices(self._h, _vp(pk.data), _vp(pk.offsets), 1, _vp(out), 0)
+        _native.check(rc, "pbf_hash_indices")
+        return [int(x) for x in out]
+
+    def add(self, key: str) -> None:
+        """bloom_filter.py:60-65 (buffered; sent as one batch at the next read)."""
+        if self.nb_hash_functions > 0:
+            self._require_modulus()
+        self._pending.append(key)
+        if len(self._pending) >= _PENDING_FLUSH:
+            self._flush()
+
+    def may_contain(self, key: str) -> bool:
+        """bloom_filter.py:67-74."""
+        return bool(self._probe_packed(PackedKeys.from_strs([key]))[0] & 1)
+
+    def to_bytes(self) -> bytes:
+        """bloom_filter.py:76-81: little-endian bitmap + one byte of k (struct.error if k > 255)."""
+        encoded_nb_hash_functions = struct.pack("B", self.nb_hash_functions)
+        return self.bitmap() + encoded_nb_hash_functions
+
+    @classmethod
+    def from_bytes(cls, data: bytes, device: Optional[int] = None) -> "BloomFilter":
+        """bloom_filter.py:83-90."""
+        nb_bytes = len(data) - 1
+        nb_hash_functions = struct.unpack("B", data[nb_bytes:])[0]
+        bf = cls(nb_bytes=nb_bytes, nb_hash_functions=nb_hash_functions, device=device)
+        if nb_bytes > 0:
+            arr = np.frombuffer(bytes(data[:nb_bytes]), dtype=np.uint8)
+            _native.check(_native.lib().pbf_set_bitmap(bf._h, _vp(arr), nb_bytes), "pbf_set_bitmap")
+        return bf
+
+    @classmethod
+    def build_from_keys_and_fp_rate(cls, keys, fp_rate: float, device: Optional[int] = None) -> "BloomFilter":
+        """bloom_filter.py:92-119 — same sizing expression order; one batched device build."""
+        n = keys.n if isinstance(keys, PackedKeys) else len(keys)
+        m = (-n * log(fp_rate)) / (log(2) ** 2)
+        k = (m / n) * log(2)
+        bloom_filter = cls(nb_bytes=ceil(m / 8), nb_hash_functions=round(k), device=device)
+        bloom_filter.add_many(keys)
+        return bloom_filter
+
+    # ------------------------------------------------------------------ batch extensions
+    def add_many(self, keys) -> None:
+        """add() for every key of `keys` (list[str] / iterable of str / PackedKeys)."""
+        pk = keys if isinstance(keys, PackedKeys) else PackedKeys.from_strs(list(keys))
+        self._add_packed(pk)
+
+    def may_contain_many(self, keys, packed: bool = False) -> np.ndarray:
+        """may_contain() for every key: bool array, or the LSB-first hit mask if packed=True."""
+        pk = keys if isinstance(keys, PackedKeys) else PackedKeys.from_strs(list(keys))
+        hm = self._probe_packed(pk)
+        if packed:
+            return hm
+        return np.unpackbits(hm, bitorder="little")[:pk.n].astype(bool)
+
+    # ------------------------------------------------------------------ device-resident batches
+    # Pointers are device addresses on self.device (e.g. torch.Tensor.data_ptr()).  These calls
+    # are asynchronous on the filter's stream: keep the buffers alive and call sync() (or wait
+    # on an event recorded on `stream`) before reading results or freeing inputs.
+    def clear(self) -> None:
+        self._pending = []
+        if self._h is not None:
+            _native.check(_native.lib().pbf_clear(self._h), "pbf_clear")
+
+    def add_device_fixed(self, keys_ptr: int, key_len: int, n: int) -> None:
+        if n and self._require_modulus():
+            self._flush()
+            _native.check(_native.lib().pbf_add_fixed(self._h, ctypes.c_void_p(keys_ptr), key_len, n, 1), "pbf_add_fixed")
+
+    def add_device(self, keys_ptr: int, offsets_ptr: int, n: int) -> None:
+        if n and self._require_modulus():
+            self._flush()
+            _native.check(_native.lib().pbf_add(self._h, ctypes.c_void_p(keys_ptr), ctypes.c_void_p(offsets_ptr), n, 1),
+                          "pbf_add")
+
+    def probe_device_fixed(self, keys_ptr: int, key_len: int, n: int, hitmask_ptr: int) -> None:
+        if n:
+            self._require_modulus()
+            self._flush()
+            _native.check(_native.lib().pbf_probe_fixed(self._h, ctypes.c_void_p(keys_ptr), key_len, n,
+                                                        ctypes.c_void_p(hitmask_ptr), 1), "pbf_probe_fixed")
+
+    def probe_device(self, keys_ptr: int, offsets_ptr: int, n: int, hitmask_ptr: int) -> None:
+        if n:
+            self._require_modulus()
+            self._flush()
+            _native.check(_native.lib().pbf_probe(self._h, ctypes.c_void_p(keys_ptr), ctypes.c_void_p(offsets_ptr), n,
+                                                  ctypes.c_void_p(hitmask_ptr), 1), "pbf_probe")
+
+    def sync(self) -> None:
+        if self._h is not None:
+            _native.check(_native.lib().pbf_sync(self._h), "pbf_sync")
+
+    @property
+    def stream(self) -> int:
+        """The filter's hipStream_t as an int (torch.cuda.ExternalStream(stream))."""
+        return 0 if self._h is None else int(_native.lib().pbf_stream(self._h) or 0)
+
+    def popcount(self) -> int:
+        if self.nb_bytes <= 0:
+            return 0
+        self._flush()
+        out = ctypes.c_uint64()
+        _native.check(_native.lib().pbf_popcount(self._h, ctypes.byref(out)), "pbf_popcount")
+        return out.value
+
+    def set_build_mode(self, mode: int) -> None:
+        if self._h is not None:
+            _native.check(_native.lib().pbf_set_build_mode(self._h, int(mode)), "pbf_set_build_mode")
+
+    @property
+    def last_build_mode(self) -> int:
+        return 0 if self._h is None else _native.lib().pbf_last_build_mode(self._h)
+
+    @property
+    def handle(self):
+        return self._h
+
+    def __repr__(self):
+        return f"BloomFilter(nb_bytes={self.nb_bytes}, nb_hash_functions={self.nb_hash_functions}, device={self.device})"

@@ -1,0 +1,159 @@
+// Device-side hashing for the bloom path: MurmurHash3_x86_32 over UTF-8 key bytes with seeds
+// 0..k-1 (mmh3.hash(key, i), reference src/bloom_filter.py:46) and the Python floor-mod
+// `hash % bits_size` (bloom_filter.py:47), for gfx950.
+//
+// A key's 4-byte blocks are mixed (k1 * c1, rotl 15, * c2) independently of the seed, so one
+// pass over the key bytes feeds all k seed states at once: the bytes are loaded once and the
+// per-block multiply pair is paid once per key, not once per seed.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace pbf {
+
+constexpr uint32_t kC1 = 0xcc9e2d51u;
+constexpr uint32_t kC2 = 0x1b873593u;
+
+__device__ __forceinline__ uint32_t rotl32(uint32_t x, int r) { return __builtin_rotateleft32(x, r); }
+
+__device__ __forceinline__ uint32_t mix_block(uint32_t k) {
+    k *= kC1;
+    k = rotl32(k, 15);
+    return k * kC2;
+}
+
+__device__ __forceinline__ uint32_t round_h(uint32_t h, uint32_t km) {
+    h ^= km;
+    h = rotl32(h, 13);
+    return h * 5u + 0xe6546b64u;
+}
+
+__device__ __forceinline__ uint32_t fmix32(uint32_t h) {
+    h ^= h >> 16;
+    h *= 0x85ebca6bu;
+    h ^= h >> 13;
+    h *= 0xc2b2ae35u;
+    h ^= h >> 16;
+    return h;
+}
+
+// Little-endian 4 bytes at an arbitrary byte address.  Only dwords that contain at least one
+// requested byte are touched, so the read never leaves the page of a valid byte.
+__device__ __forceinline__ uint32_t load_u32_any(const uint8_t* p) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    const uint32_t* q = reinterpret_cast<const uint32_t*>(a & ~uintptr_t(3));
+    const uint32_t sh = uint32_t(a & 3);
+    const uint32_t lo = q[0];
+    if (sh == 0) return lo;
+    const uint32_t hi = q[1];
+    return __builtin_amdgcn_alignbyte(hi, lo, sh);
+}
+
+// The t (1..3) tail bytes at p, zero-extended, little-endian (MurmurHash3 tail block).
+__device__ __forceinline__ uint32_t load_tail(const uint8_t* p, uint32_t t) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    const uint32_t* q = reinterpret_cast<const uint32_t*>(a & ~uintptr_t(3));
+    const uint32_t sh = uint32_t(a & 3);
+    const uint32_t lo = q[0];
+    const uint32_t hi = (sh + t > 4) ? q[1] : 0u;
+    const uint32_t v = __builtin_amdgcn_alignbyte(hi, lo, sh);
+    return v & ((1u << (8 * t)) - 1u);
+}
+
+// All k seeds of MurmurHash3_x86_32 for one key; emit(seed, hash_u32) is called for
+// seed = 0..k-1.  KMAX is the compile-time register budget for seed states (k <= KMAX).
+template <int KMAX, class Emit>
+__device__ __forceinline__ void murmur_seeds(const uint8_t* p, uint32_t len, int k, Emit&& emit) {
+    uint32_t h[KMAX];
+#pragma unroll
+    for (int s = 0; s < KMAX; ++s) h[s] = uint32_t(s);
+    const uint32_t nb = len >> 2;
+    const bool aligned = (reinterpret_cast<uintptr_t>(p) & 3) == 0;
+    if (aligned) {
+        const uint32_t* q = reinterpret_cast<const uint32_t*>(p);
+        for (uint32_t b = 0; b < nb; ++b) {
+            const uint32_t km = mix_block(q[b]);
+#pragma unroll
+            for (int s = 0; s < KMAX; ++s) h[s] = round_h(h[s], km);
+        }
+    } else {
+        for (uint32_t b = 0; b < nb; ++b) {
+            const uint32_t km = mix_block(load_u32_any(p + 4 * b));
+#pragma unroll
+            for (int s = 0; s < KMAX; ++s) h[s] = round_h(h[s], km);
+        }
+    }
+    const uint32_t t = len & 3;
+    if (t) {
+        const uint32_t km = mix_block(load_tail(p + 4 * nb, t));
+#pragma unroll
+        for (int s = 0; s < KMAX; ++s) h[s] ^= km;
+    }
+#pragma unroll
+    for (int s = 0; s < KMAX; ++s)
+        if (s < k) emit(s, fmix32(h[s] ^ len));
+}
+
+// Fixed 16-byte keys from one 16-byte load (the C2/C4/C5 key shape).
+template <int KMAX, class Emit>
+__device__ __forceinline__ void murmur_seeds16(uint4 w, int k, Emit&& emit) {
+    const uint32_t m0 = mix_block(w.x), m1 = mix_block(w.y), m2 = mix_block(w.z), m3 = mix_block(w.w);
+#pragma unroll
+    for (int s = 0; s < KMAX; ++s) {
+        if (s < k) {
+            uint32_t h = uint32_t(s);
+            h = round_h(h, m0);
+            h = round_h(h, m1);
+            h = round_h(h, m2);
+            h = round_h(h, m3);
+            emit(s, fmix32(h ^ 16u));
+        }
+    }
+}
+
+// Runtime-k fallback (k > 32): one seed at a time, key bytes re-read (from L1) per seed.
+template <class Emit>
+__device__ __forceinline__ void murmur_seeds_loop(const uint8_t* p, uint32_t len, int k, Emit&& emit) {
+    const uint32_t nb = len >> 2;
+    const uint32_t t = len & 3;
+    for (int s = 0; s < k; ++s) {
+        uint32_t h = uint32_t(s);
+        for (uint32_t b = 0; b < nb; ++b) h = round_h(h, mix_block(load_u32_any(p + 4 * b)));
+        if (t) h ^= mix_block(load_tail(p + 4 * nb, t));
+        emit(s, fmix32(h ^ len));
+    }
+}
+
+// ---------------------------------------------------------------- Python floor-mod index
+// idx = h % m with h the SIGNED int32 hash and Python's floor semantics (result in [0, m)).
+enum IndexMode : uint32_t {
+    kPow2 = 0,   // m a power of two, m <= 2^32: idx = u32(h) & (m-1)
+    kSmall = 1,  // m < 2^31: a = h>=0 ? h : ~h (< 2^31); r = a mod m; idx = h>=0 ? r : m-1-r
+    kLarge = 2,  // m >= 2^31: |h| <= 2^31 <= m, so idx = h>=0 ? h : h + m (64-bit)
+};
+
+struct IndexMap {
+    uint64_t m;      // bits_size = 8 * nb_bytes
+    uint64_t magic;  // Lemire fastmod constant for kSmall: floor((2^64-1)/m) + 1
+    uint32_t mode;
+    uint32_t mask;   // m-1 for kPow2
+};
+
+// a mod d for a, d < 2^32 (Lemire, Kaser & Kurz, "Faster remainder by direct computation").
+__device__ __forceinline__ uint32_t fastmod_u32(uint32_t a, uint64_t magic, uint32_t d) {
+    const uint64_t low = magic * uint64_t(a);
+    return uint32_t(__umul64hi(low, uint64_t(d)));
+}
+
+__device__ __forceinline__ uint64_t py_index(uint32_t hu, const IndexMap& im) {
+    const int32_t h = int32_t(hu);
+    if (im.mode == kPow2) return uint64_t(hu & im.mask);
+    if (im.mode == kSmall) {
+        const uint32_t a = h >= 0 ? hu : ~hu;
+        const uint32_t r = fastmod_u32(a, im.magic, uint32_t(im.m));
+        return h >= 0 ? uint64_t(r) : uint64_t(uint32_t(im.m) - 1u - r);
+    }
+    return h >= 0 ? uint64_t(hu) : uint64_t(int64_t(h) + int64_t(im.m));
+}
+
+}  // namespace pbf

@@ -1,0 +1,730 @@
+// libpebblebloom.so — C-ABI (include/pebblebloom.h) over the HIP bloom kernels.
+//
+// Reference surface replaced: MaudGautier/pebbledb src/bloom_filter.py —
+//   pbf_create        ← BloomFilter.__init__            (bloom_filter.py:26-31)
+//   pbf_add[_fixed]   ← BloomFilter.add / _set_bit       (:60-65, :51-54)
+//   pbf_probe[_fixed] ← BloomFilter.may_contain / _is_bit_set (:67-74, :56-58)
+//   pbf_hash_indices  ← BloomFilter._hash                (:38-49)
+//   pbf_get_bitmap    ← BloomFilter.to_bytes (bitmap part) (:76-81)
+//   pbf_set_bitmap    ← BloomFilter.from_bytes (bitmap part) (:83-90)
+// There is no CPU fallback in this library: every entry point runs on the GPU or fails.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <type_traits>
+
+#include "../../include/pebblebloom.h"
+#include "bloom_kernels.hpp"
+
+using namespace pbf;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& msg) {
+    g_last_error = msg;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                          \
+    do {                                                                                       \
+        hipError_t e_ = (expr);                                                                \
+        if (e_ != hipSuccess)                                                                  \
+            return fail(PBF_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));       \
+    } while (0)
+
+#define CHECK_LAUNCH() HIP_TRY(hipGetLastError())
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    hipError_t ensure(size_t want) {
+        if (want <= bytes) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+        hipError_t e = hipMalloc(&p, want);
+        if (e == hipSuccess) bytes = want;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+};
+
+struct PinBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    hipEvent_t done = nullptr;  // last async copy out of this buffer
+    hipError_t ensure(size_t want) {
+        if (want <= bytes) return hipSuccess;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        bytes = 0;
+        hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+        if (e == hipSuccess) bytes = want;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipHostFree(p);
+        if (done) (void)hipEventDestroy(done);
+        p = nullptr;
+        done = nullptr;
+        bytes = 0;
+    }
+};
+
+// host→device staging chunk (PBF_STAGE_BYTES overrides, for tests of the chunked path)
+size_t stage_bytes() {
+    static const size_t v = [] {
+        const char* e = std::getenv("PBF_STAGE_BYTES");
+        const long long x = e ? std::atoll(e) : 0;
+        return x > 0 ? size_t(x) : (size_t(256) << 20);
+    }();
+    return v;
+}
+constexpr uint64_t kMaxPositions = uint64_t(1) << 30; // tiled pipeline batch (4 GiB of positions)
+
+int kmax_for(uint32_t k) {
+    if (k <= 4) return 4;
+    if (k <= 8) return 8;
+    if (k <= 16) return 16;
+    if (k <= 32) return 32;
+    return 0;
+}
+
+template <class F>
+void dispatch(int kmax, int km, F&& f) {
+    auto g = [&](auto KM) {
+        switch (kmax) {
+            case 4: f(std::integral_constant<int, 4>{}, KM); break;
+            case 8: f(std::integral_constant<int, 8>{}, KM); break;
+            case 16: f(std::integral_constant<int, 16>{}, KM); break;
+            case 32: f(std::integral_constant<int, 32>{}, KM); break;
+            default: f(std::integral_constant<int, 0>{}, KM); break;
+        }
+    };
+    switch (km) {
+        case kFixed16: g(std::integral_constant<int, kFixed16>{}); break;
+        case kFixedN: g(std::integral_constant<int, kFixedN>{}); break;
+        default: g(std::integral_constant<int, kVar>{}); break;
+    }
+}
+
+IndexMap make_index_map(uint64_t m) {
+    IndexMap im{};
+    im.m = m;
+    const bool pow2 = (m & (m - 1)) == 0;
+    if (pow2 && m <= (uint64_t(1) << 32)) {
+        im.mode = kPow2;
+        im.mask = uint32_t(m - 1);
+    } else if (m < (uint64_t(1) << 31)) {
+        im.mode = kSmall;
+        im.magic = ~uint64_t(0) / m + 1;
+    } else {
+        im.mode = kLarge;
+    }
+    return im;
+}
+
+// Dynamic LDS above 64 KiB must be allowed per kernel (gfx950 has 160 KiB per CU).
+template <class K>
+hipError_t allow_lds(K kernel, size_t bytes) {
+    if (bytes <= 65536) return hipSuccess;
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                               int(bytes));
+}
+
+uint32_t ceil_log2(uint64_t x) {
+    uint32_t r = 0;
+    while ((uint64_t(1) << r) < x) ++r;
+    return r;
+}
+
+}  // namespace
+
+struct pbf_filter {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    uint64_t nb_bytes = 0;
+    uint32_t k = 0;
+    uint64_t words = 0;  // logical words ceil(nb_bytes / 4)
+    uint64_t alloc_words = 0;
+    uint32_t* bitmap = nullptr;
+    bool pristine = true;  // logically all-zero; reachable words not yet materialised
+    bool middle_dirty = false;  // m > 2^32: unreachable middle written by set_bitmap
+    int mode = PBF_BUILD_AUTO;
+    int last_mode = 0;
+    IndexMap im{};
+    TileMap tm{};
+    bool tiled_ok = false;
+    DevBuf positions, counts, total, base;
+    DevBuf dkeys, doffs, dout;
+    PinBuf pin[2];
+    int pin_next = 0;
+    uint64_t* dpop = nullptr;
+};
+
+namespace {
+
+int enter(pbf_filter_t* f) {
+    if (!f) return fail(PBF_ERR_INVALID, "null filter handle");
+    HIP_TRY(hipSetDevice(f->device));
+    return PBF_OK;
+}
+
+// Bring a pristine bitmap to its explicit all-zero form (before atomics / reads).
+int materialise(pbf_filter_t* f) {
+    if (!f->pristine) return PBF_OK;
+    HIP_TRY(hipMemsetAsync(f->bitmap, 0, f->alloc_words * 4, f->stream));
+    f->pristine = false;
+    return PBF_OK;
+}
+
+struct Batch {
+    KeySet ks;
+    int km;
+    uint64_t n;
+};
+
+Batch make_batch(const uint8_t* keys, const uint64_t* offsets, uint32_t key_len, uint64_t n) {
+    Batch b{};
+    b.ks.data = keys;
+    b.ks.offsets = offsets;
+    b.ks.off0 = offsets;
+    b.ks.key_len = key_len;
+    b.n = n;
+    if (offsets)
+        b.km = kVar;
+    else if (key_len == 16 && (reinterpret_cast<uintptr_t>(keys) & 15) == 0)
+        b.km = kFixed16;
+    else
+        b.km = kFixedN;
+    return b;
+}
+
+uint32_t grid_for(uint64_t n, uint32_t block, uint32_t cap = 16384) {
+    uint64_t g = (n + block - 1) / block;
+    return uint32_t(std::max<uint64_t>(1, std::min<uint64_t>(g, cap)));
+}
+
+int run_atomic(pbf_filter_t* f, const Batch& b) {
+    int rc = materialise(f);
+    if (rc) return rc;
+    const uint32_t grid = grid_for(b.n, 256);
+    dispatch(kmax_for(f->k), b.km, [&](auto KMAX, auto KM) {
+        k_build_atomic<decltype(KMAX)::value, decltype(KM)::value>
+            <<<grid, 256, 0, f->stream>>>(b.ks, b.n, int(f->k), f->im, f->bitmap);
+    });
+    CHECK_LAUNCH();
+    return PBF_OK;
+}
+
+// Scatter-kernel geometry for B tiles: (workgroups, keys per sub-chunk, LDS bytes).
+void scatter_geometry(uint32_t B, uint32_t k, uint64_t n, uint32_t* G, uint32_t* keys_per_sub, size_t* lds) {
+    const size_t fixed = size_t(3 * B + 1 + 16) * 4;
+    // Two workgroups per CU (<= 78 KiB each) while that leaves >= 12K staged positions,
+    // otherwise one (<= 156 KiB).
+    size_t budget = 78 * 1024;
+    uint32_t per_cu = 2;
+    if (budget < fixed + 12288 * 4) {
+        budget = 156 * 1024;
+        per_cu = 1;
+    }
+    const uint64_t stage = (budget - fixed) / 4;
+    const uint32_t kps = uint32_t(std::max<uint64_t>(1, stage / k));
+    *keys_per_sub = kps;
+    *lds = fixed + size_t(kps) * k * 4;
+    const uint64_t want = 256ull * per_cu;
+    const uint64_t by_n = std::max<uint64_t>(1, (n + 2047) / 2048);
+    *G = uint32_t(std::min(want, by_n));
+}
+
+int run_tiled(pbf_filter_t* f, const Batch& b) {
+    const TileMap& tm = f->tm;
+    const uint32_t B = tm.nbuckets;
+    const uint32_t k = f->k;
+    uint32_t G, kps;
+    size_t lds_scatter;
+    scatter_geometry(B, k, b.n, &G, &kps, &lds_scatter);
+    const uint64_t kpw = (b.n + G - 1) / G;
+    const uint64_t npos = b.n * k;
+    HIP_TRY(f->positions.ensure(std::max<uint64_t>(npos, 1) * 4));
+    HIP_TRY(f->counts.ensure(size_t(G) * B * 4));
+    HIP_TRY(f->total.ensure(size_t(B) * 4));
+    HIP_TRY(f->base.ensure(size_t(B + 1) * 4));
+    auto* counts = static_cast<uint32_t*>(f->counts.p);
+    auto* total = static_cast<uint32_t*>(f->total.p);
+    auto* base = static_cast<uint32_t*>(f->base.p);
+    auto* pos = static_cast<uint32_t*>(f->positions.p);
+    hipStream_t s = f->stream;
+    hipError_t err = hipSuccess;
+    dispatch(kmax_for(k), b.km, [&](auto KMAX, auto KM) {
+        auto kern = k_hist<decltype(KMAX)::value, decltype(KM)::value>;
+        err = allow_lds(kern, size_t(B) * 4);
+        if (err == hipSuccess) kern<<<G, 1024, size_t(B) * 4, s>>>(b.ks, b.n, int(k), tm, kpw, counts);
+    });
+    HIP_TRY(err);
+    CHECK_LAUNCH();
+    k_colscan<<<(B + 63) / 64, 1024, 0, s>>>(counts, G, B, total);
+    CHECK_LAUNCH();
+    const size_t lds_base = size_t(2 * B + 1 + 16) * 4;
+    HIP_TRY(allow_lds(k_basescan, lds_base));
+    k_basescan<<<1, 1024, lds_base, s>>>(total, B, base);
+    CHECK_LAUNCH();
+    dispatch(kmax_for(k), b.km, [&](auto KMAX, auto KM) {
+        auto kern = k_scatter<decltype(KMAX)::value, decltype(KM)::value>;
+        err = allow_lds(kern, lds_scatter);
+        if (err == hipSuccess) kern<<<G, 1024, lds_scatter, s>>>(b.ks, b.n, int(k), tm, kpw, kps, counts, base, pos);
+    });
+    HIP_TRY(err);
+    CHECK_LAUNCH();
+    const size_t lds_tile = (size_t(1) << tm.tb) / 8;
+    HIP_TRY(allow_lds(k_tile, lds_tile));
+    k_tile<<<B, 1024, lds_tile, s>>>(pos, base, tm, f->bitmap, f->pristine ? 1 : 0);
+    CHECK_LAUNCH();
+    f->pristine = false;
+    return PBF_OK;
+}
+
+bool want_tiled(pbf_filter_t* f, uint64_t n) {
+    if (!f->tiled_ok || f->k == 0 || f->k > 32) return false;
+    if (f->mode == PBF_BUILD_TILED) return true;
+    if (f->mode == PBF_BUILD_ATOMIC) return false;
+    const uint64_t npos = n * f->k;
+    // the tile pass streams the whole bitmap once (twice when not pristine); random atomics
+    // cost ~16x a streamed position.  Tiles win once positions are a small fraction of it.
+    const uint64_t bitmap_bytes = f->words * 4 * (f->pristine ? 1 : 2);
+    return npos >= (uint64_t(1) << 16) && npos * 64 >= bitmap_bytes;
+}
+
+int add_device(pbf_filter_t* f, const Batch& b) {
+    if (b.n == 0 || f->k == 0) return PBF_OK;
+    if (want_tiled(f, b.n)) {
+        // positions are indexed by u32 inside one pipeline: batch very large inputs
+        const uint64_t per = std::max<uint64_t>(1, kMaxPositions / f->k);
+        for (uint64_t i0 = 0; i0 < b.n; i0 += per) {
+            Batch c = b;
+            c.n = std::min<uint64_t>(per, b.n - i0);
+            if (b.km == kVar)
+                c.ks.offsets = b.ks.offsets + i0;  // off0 unchanged: offsets stay relative to it
+            else
+                c.ks.data = b.ks.data + i0 * b.ks.key_len;
+            int rc = run_tiled(f, c);
+            if (rc) return rc;
+        }
+        f->last_mode = PBF_BUILD_TILED;
+        return PBF_OK;
+    }
+    f->last_mode = PBF_BUILD_ATOMIC;
+    return run_atomic(f, b);
+}
+
+int probe_device(pbf_filter_t* f, const Batch& b, uint8_t* hitmask_dev) {
+    if (b.n == 0) return PBF_OK;
+    int rc = materialise(f);
+    if (rc) return rc;
+    const uint32_t grid = grid_for(b.n, 256, 1u << 20);
+    dispatch(kmax_for(f->k), b.km, [&](auto KMAX, auto KM) {
+        k_probe<decltype(KMAX)::value, decltype(KM)::value>
+            <<<grid, 256, 0, f->stream>>>(b.ks, b.n, int(f->k), f->im, f->bitmap, hitmask_dev);
+    });
+    CHECK_LAUNCH();
+    return PBF_OK;
+}
+
+int hash_device(pbf_filter_t* f, const Batch& b, uint64_t* out_dev) {
+    if (b.n == 0 || f->k == 0) return PBF_OK;
+    const uint32_t grid = grid_for(b.n, 256);
+    dispatch(kmax_for(f->k), b.km, [&](auto KMAX, auto KM) {
+        k_hash_indices<decltype(KMAX)::value, decltype(KM)::value>
+            <<<grid, 256, 0, f->stream>>>(b.ks, b.n, int(f->k), f->im, out_dev);
+    });
+    CHECK_LAUNCH();
+    return PBF_OK;
+}
+
+// Host-resident keys: stream them through pinned double buffers in chunks of whole keys.
+// `op(batch_on_device, first_key_index)` runs the device work for one chunk.
+template <class Op>
+int for_host_chunks(pbf_filter_t* f, const uint8_t* keys, const uint64_t* offsets, uint32_t key_len, uint64_t n,
+                    uint64_t key_align, Op&& op) {
+    uint64_t i0 = 0;
+    while (i0 < n) {
+        // choose [i0, i1)
+        uint64_t i1;
+        if (offsets) {
+            // largest i1 with bytes <= stage_bytes() (at least one key)
+            uint64_t lo = i0 + 1, hi = n;
+            const uint64_t start = offsets[i0];
+            if (offsets[n] - start <= stage_bytes()) {
+                i1 = n;
+            } else {
+                while (lo < hi) {
+                    uint64_t mid = (lo + hi + 1) / 2;
+                    if (offsets[mid] - start <= stage_bytes()) lo = mid; else hi = mid - 1;
+                }
+                i1 = lo;
+                if (i1 - i0 > key_align) i1 = i0 + ((i1 - i0) / key_align) * key_align;
+            }
+        } else {
+            uint64_t per = std::max<uint64_t>(1, stage_bytes() / std::max<uint32_t>(1, key_len));
+            per = std::max<uint64_t>(key_align, (per / key_align) * key_align);
+            i1 = std::min<uint64_t>(n, i0 + per);
+        }
+        const uint64_t cn = i1 - i0;
+        const uint64_t byte0 = offsets ? offsets[i0] : i0 * key_len;
+        const uint64_t nbytes = offsets ? offsets[i1] - offsets[i0] : cn * key_len;
+        const size_t off_bytes = offsets ? size_t(cn + 1) * 8 : 0;
+        PinBuf& pb = f->pin[f->pin_next];
+        f->pin_next ^= 1;
+        if (pb.done) HIP_TRY(hipEventSynchronize(pb.done));
+        HIP_TRY(pb.ensure(nbytes + off_bytes + 16));
+        if (!pb.done) HIP_TRY(hipEventCreateWithFlags(&pb.done, hipEventDisableTiming));
+        // device staging (single buffer: stream order serialises reuse)
+        HIP_TRY(f->dkeys.ensure(((nbytes + 15) & ~uint64_t(15)) + 16));
+        if (offsets) HIP_TRY(f->doffs.ensure(off_bytes));
+        std::memcpy(pb.p, keys + byte0, nbytes);
+        if (offsets) std::memcpy(static_cast<uint8_t*>(pb.p) + ((nbytes + 15) & ~uint64_t(15)), offsets + i0, off_bytes);
+        HIP_TRY(hipMemcpyAsync(f->dkeys.p, pb.p, nbytes, hipMemcpyHostToDevice, f->stream));
+        if (offsets)
+            HIP_TRY(hipMemcpyAsync(f->doffs.p, static_cast<uint8_t*>(pb.p) + ((nbytes + 15) & ~uint64_t(15)), off_bytes,
+                                   hipMemcpyHostToDevice, f->stream));
+        HIP_TRY(hipEventRecord(pb.done, f->stream));
+        Batch b = make_batch(static_cast<const uint8_t*>(f->dkeys.p),
+                             offsets ? static_cast<const uint64_t*>(f->doffs.p) : nullptr, key_len, cn);
+        int rc = op(b, i0);
+        if (rc) return rc;
+        i0 = i1;
+    }
+    return PBF_OK;
+}
+
+int check_keys(pbf_filter_t* f, const uint8_t* keys, const uint64_t* offsets, uint32_t key_len, uint64_t n,
+               bool var) {
+    int rc = enter(f);
+    if (rc) return rc;
+    if (n == 0) return PBF_OK;
+    if (!keys) return fail(PBF_ERR_INVALID, "null keys pointer");
+    if (var && !offsets) return fail(PBF_ERR_INVALID, "variable-length keys need offsets[n+1]");
+    if (!var && key_len == 0) {
+        // zero-length fixed keys are legal (key ""), handled through the variable path below
+    }
+    return PBF_OK;
+}
+
+int add_impl(pbf_filter_t* f, const uint8_t* keys, const uint64_t* offsets, uint32_t key_len, uint64_t n,
+             int on_device) {
+    int rc = check_keys(f, keys, offsets, key_len, n, offsets != nullptr);
+    if (rc || n == 0) return rc;
+    if (on_device) {
+        return add_device(f, make_batch(keys, offsets, key_len, n));
+    }
+    rc = for_host_chunks(f, keys, offsets, key_len, n, 1, [&](const Batch& b, uint64_t) { return add_device(f, b); });
+    if (rc) return rc;
+    HIP_TRY(hipStreamSynchronize(f->stream));
+    return PBF_OK;
+}
+
+int probe_impl(pbf_filter_t* f, const uint8_t* keys, const uint64_t* offsets, uint32_t key_len, uint64_t n,
+               uint8_t* hitmask, int on_device) {
+    int rc = check_keys(f, keys, offsets, key_len, n, offsets != nullptr);
+    if (rc || n == 0) return rc;
+    if (!hitmask) return fail(PBF_ERR_INVALID, "null hitmask");
+    if (on_device) {
+        return probe_device(f, make_batch(keys, offsets, key_len, n), hitmask);
+    }
+    rc = for_host_chunks(f, keys, offsets, key_len, n, 64, [&](const Batch& b, uint64_t i0) {
+        HIP_TRY(f->dout.ensure((b.n + 7) / 8 + 8));
+        int r = probe_device(f, b, static_cast<uint8_t*>(f->dout.p));
+        if (r) return r;
+        HIP_TRY(hipMemcpyAsync(hitmask + i0 / 8, f->dout.p, (b.n + 7) / 8, hipMemcpyDeviceToHost, f->stream));
+        HIP_TRY(hipStreamSynchronize(f->stream));
+        return PBF_OK;
+    });
+    if (rc) return rc;
+    HIP_TRY(hipStreamSynchronize(f->stream));
+    return PBF_OK;
+}
+
+int hash_impl(pbf_filter_t* f, const uint8_t* keys, const uint64_t* offsets, uint32_t key_len, uint64_t n,
+              uint64_t* out, int on_device) {
+    int rc = check_keys(f, keys, offsets, key_len, n, offsets != nullptr);
+    if (rc || n == 0) return rc;
+    if (!out) return fail(PBF_ERR_INVALID, "null output");
+    if (on_device) return hash_device(f, make_batch(keys, offsets, key_len, n), out);
+    rc = for_host_chunks(f, keys, offsets, key_len, n, 1, [&](const Batch& b, uint64_t i0) {
+        HIP_TRY(f->dout.ensure(b.n * f->k * 8 + 8));
+        int r = hash_device(f, b, static_cast<uint64_t*>(f->dout.p));
+        if (r) return r;
+        HIP_TRY(hipMemcpyAsync(out + i0 * f->k, f->dout.p, b.n * f->k * 8, hipMemcpyDeviceToHost, f->stream));
+        HIP_TRY(hipStreamSynchronize(f->stream));
+        return PBF_OK;
+    });
+    if (rc) return rc;
+    HIP_TRY(hipStreamSynchronize(f->stream));
+    return PBF_OK;
+}
+
+__global__ void k_popcount(const uint32_t* __restrict__ w, uint64_t n, unsigned long long* out) {
+    __shared__ unsigned long long part[4];
+    unsigned long long s = 0;
+    const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+    for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) s += __popc(w[i]);
+    for (int d = 32; d > 0; d >>= 1) s += __shfl_down(s, d, 64);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) atomicAdd(out, part[0] + part[1] + part[2] + part[3]);
+}
+
+}  // namespace
+
+extern "C" {
+
+int pbf_version(void) { return 100; }
+
+int pbf_device_count(int* count) {
+    if (!count) return fail(PBF_ERR_INVALID, "null count");
+    HIP_TRY(hipGetDeviceCount(count));
+    return PBF_OK;
+}
+
+const char* pbf_last_error(void) { return g_last_error.c_str(); }
+
+int pbf_create(int device, uint64_t nb_bytes, uint32_t nb_hash_functions, pbf_filter_t** out) {
+    if (!out) return fail(PBF_ERR_INVALID, "null out");
+    *out = nullptr;
+    if (nb_bytes == 0) return fail(PBF_ERR_ZERO_SIZE, "nb_bytes == 0 (integer modulo by zero)");
+    HIP_TRY(hipSetDevice(device));
+    auto* f = new pbf_filter();
+    f->device = device;
+    f->nb_bytes = nb_bytes;
+    f->k = nb_hash_functions;
+    f->words = (nb_bytes + 3) / 4;
+    f->alloc_words = (f->words + 3) & ~uint64_t(3);
+    const uint64_t m = nb_bytes * 8;
+    f->im = make_index_map(m);
+    // tile geometry
+    const bool cspace = m > (uint64_t(1) << 32);
+    const uint64_t P = cspace ? (uint64_t(1) << 32) : m;
+    TileMap tm{};
+    tm.im = f->im;
+    tm.tb = std::min<uint32_t>(20, std::max<uint32_t>(10, ceil_log2(P)));
+    tm.nbuckets = uint32_t((P + (uint64_t(1) << tm.tb) - 1) >> tm.tb);
+    tm.cspace = cspace ? 1 : 0;
+    tm.total_words = f->words;
+    f->tiled_ok = true;
+    if (cspace) {
+        const uint64_t delta = m - (uint64_t(1) << 32);
+        if (delta % 32) f->tiled_ok = false;
+        tm.delta_words = delta / 32;
+    }
+    if (tm.nbuckets > 8192) f->tiled_ok = false;  // LDS budget of k_scatter
+    f->tm = tm;
+    hipError_t e = hipStreamCreateWithFlags(&f->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipMalloc(&f->bitmap, f->alloc_words * 4);
+    if (e == hipSuccess) e = hipMalloc(&f->dpop, 8);
+    // The tiled build writes every reachable word itself; the unreachable middle of a
+    // m > 2^32 filter is zeroed once here.  Otherwise start from an explicit zero bitmap.
+    if (e == hipSuccess) {
+        if (f->tiled_ok && cspace) {
+            const uint64_t lo_w = (uint64_t(1) << 31) / 32;
+            const uint64_t hi_w = tm.delta_words + lo_w;  // first word of [m - 2^31, m)
+            if (hi_w > lo_w) e = hipMemsetAsync(f->bitmap + lo_w, 0, (hi_w - lo_w) * 4, f->stream);
+            f->pristine = true;
+        } else {
+            e = hipMemsetAsync(f->bitmap, 0, f->alloc_words * 4, f->stream);
+            f->pristine = false;
+        }
+    }
+    if (e == hipSuccess && !f->tiled_ok) f->pristine = false;
+    if (e != hipSuccess) {
+        std::string msg = std::string("pbf_create: ") + hipGetErrorString(e);
+        pbf_destroy(f);
+        return fail(PBF_ERR_HIP, msg);
+    }
+    *out = f;
+    return PBF_OK;
+}
+
+int pbf_destroy(pbf_filter_t* f) {
+    if (!f) return PBF_OK;
+    (void)hipSetDevice(f->device);
+    if (f->stream) (void)hipStreamSynchronize(f->stream);
+    if (f->bitmap) (void)hipFree(f->bitmap);
+    if (f->dpop) (void)hipFree(f->dpop);
+    f->positions.release();
+    f->counts.release();
+    f->total.release();
+    f->base.release();
+    f->dkeys.release();
+    f->doffs.release();
+    f->dout.release();
+    f->pin[0].release();
+    f->pin[1].release();
+    if (f->stream) (void)hipStreamDestroy(f->stream);
+    delete f;
+    return PBF_OK;
+}
+
+int pbf_clear(pbf_filter_t* f) {
+    int rc = enter(f);
+    if (rc) return rc;
+    if (f->tiled_ok) {
+        // The next tiled build rewrites every reachable word; a read or an atomic build
+        // materialises the zero bitmap first.  Only a from_bytes() can have dirtied the
+        // unreachable middle of an m > 2^32 filter.
+        if (f->tm.cspace && f->middle_dirty) {
+            const uint64_t lo_w = (uint64_t(1) << 31) / 32;
+            const uint64_t hi_w = f->tm.delta_words + lo_w;
+            HIP_TRY(hipMemsetAsync(f->bitmap + lo_w, 0, (hi_w - lo_w) * 4, f->stream));
+            f->middle_dirty = false;
+        }
+        f->pristine = true;
+        return PBF_OK;
+    }
+    HIP_TRY(hipMemsetAsync(f->bitmap, 0, f->alloc_words * 4, f->stream));
+    f->pristine = false;
+    return PBF_OK;
+}
+
+int pbf_add_fixed(pbf_filter_t* f, const uint8_t* keys, uint32_t key_len, uint64_t n, int on_device) {
+    if (key_len == 0 && n > 0) {
+        // n empty keys: the variable-length path with all-equal offsets
+        int rc = enter(f);
+        if (rc) return rc;
+        if (f->k == 0) return PBF_OK;
+        HIP_TRY(f->doffs.ensure((n + 1) * 8));
+        HIP_TRY(hipMemsetAsync(f->doffs.p, 0, (n + 1) * 8, f->stream));
+        HIP_TRY(f->dkeys.ensure(16));
+        rc = add_device(f, make_batch(static_cast<const uint8_t*>(f->dkeys.p),
+                                      static_cast<const uint64_t*>(f->doffs.p), 0, n));
+        if (rc) return rc;
+        if (!on_device) HIP_TRY(hipStreamSynchronize(f->stream));
+        return PBF_OK;
+    }
+    return add_impl(f, keys, nullptr, key_len, n, on_device);
+}
+
+int pbf_add(pbf_filter_t* f, const uint8_t* keys, const uint64_t* offsets, uint64_t n, int on_device) {
+    if (!offsets && n > 0) return fail(PBF_ERR_INVALID, "null offsets");
+    return add_impl(f, keys ? keys : reinterpret_cast<const uint8_t*>(offsets), offsets, 0, n, on_device);
+}
+
+int pbf_probe_fixed(pbf_filter_t* f, const uint8_t* keys, uint32_t key_len, uint64_t n, uint8_t* hitmask,
+                    int on_device) {
+    if (key_len == 0 && n > 0) return fail(PBF_ERR_INVALID, "key_len 0: use pbf_probe with offsets");
+    return probe_impl(f, keys, nullptr, key_len, n, hitmask, on_device);
+}
+
+int pbf_probe(pbf_filter_t* f, const uint8_t* keys, const uint64_t* offsets, uint64_t n, uint8_t* hitmask,
+              int on_device) {
+    if (!offsets && n > 0) return fail(PBF_ERR_INVALID, "null offsets");
+    return probe_impl(f, keys ? keys : reinterpret_cast<const uint8_t*>(offsets), offsets, 0, n, hitmask, on_device);
+}
+
+int pbf_hash_indices_fixed(pbf_filter_t* f, const uint8_t* keys, uint32_t key_len, uint64_t n, uint64_t* out,
+                           int on_device) {
+    if (key_len == 0 && n > 0) return fail(PBF_ERR_INVALID, "key_len 0: use pbf_hash_indices with offsets");
+    return hash_impl(f, keys, nullptr, key_len, n, out, on_device);
+}
+
+int pbf_hash_indices(pbf_filter_t* f, const uint8_t* keys, const uint64_t* offsets, uint64_t n, uint64_t* out,
+                     int on_device) {
+    if (!offsets && n > 0) return fail(PBF_ERR_INVALID, "null offsets");
+    return hash_impl(f, keys ? keys : reinterpret_cast<const uint8_t*>(offsets), offsets, 0, n, out, on_device);
+}
+
+int pbf_get_bitmap(pbf_filter_t* f, uint8_t* out, uint64_t nb_bytes) {
+    int rc = enter(f);
+    if (rc) return rc;
+    if (nb_bytes != f->nb_bytes) return fail(PBF_ERR_INVALID, "nb_bytes mismatch");
+    if (!out) return fail(PBF_ERR_INVALID, "null out");
+    rc = materialise(f);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(out, f->bitmap, nb_bytes, hipMemcpyDeviceToHost, f->stream));
+    HIP_TRY(hipStreamSynchronize(f->stream));
+    return PBF_OK;
+}
+
+int pbf_set_bitmap(pbf_filter_t* f, const uint8_t* in, uint64_t nb_bytes) {
+    int rc = enter(f);
+    if (rc) return rc;
+    if (nb_bytes != f->nb_bytes) return fail(PBF_ERR_INVALID, "nb_bytes mismatch");
+    if (!in) return fail(PBF_ERR_INVALID, "null input");
+    if (f->alloc_words * 4 > nb_bytes)
+        HIP_TRY(hipMemsetAsync(reinterpret_cast<uint8_t*>(f->bitmap) + nb_bytes, 0, f->alloc_words * 4 - nb_bytes,
+                               f->stream));
+    HIP_TRY(hipMemcpyAsync(f->bitmap, in, nb_bytes, hipMemcpyHostToDevice, f->stream));
+    HIP_TRY(hipStreamSynchronize(f->stream));
+    f->pristine = false;
+    f->middle_dirty = f->tm.cspace != 0;
+    return PBF_OK;
+}
+
+int pbf_popcount(pbf_filter_t* f, uint64_t* out) {
+    int rc = enter(f);
+    if (rc) return rc;
+    if (!out) return fail(PBF_ERR_INVALID, "null out");
+    rc = materialise(f);
+    if (rc) return rc;
+    HIP_TRY(hipMemsetAsync(f->dpop, 0, 8, f->stream));
+    k_popcount<<<grid_for(f->alloc_words, 256, 4096), 256, 0, f->stream>>>(
+        f->bitmap, f->alloc_words, reinterpret_cast<unsigned long long*>(f->dpop));
+    CHECK_LAUNCH();
+    HIP_TRY(hipMemcpyAsync(out, f->dpop, 8, hipMemcpyDeviceToHost, f->stream));
+    HIP_TRY(hipStreamSynchronize(f->stream));
+    return PBF_OK;
+}
+
+int pbf_sync(pbf_filter_t* f) {
+    int rc = enter(f);
+    if (rc) return rc;
+    HIP_TRY(hipStreamSynchronize(f->stream));
+    return PBF_OK;
+}
+
+void* pbf_stream(pbf_filter_t* f) { return f ? static_cast<void*>(f->stream) : nullptr; }
+void* pbf_device_bitmap(pbf_filter_t* f) {
+    if (!f) return nullptr;
+    if (materialise(f)) return nullptr;
+    return f->bitmap;
+}
+
+int pbf_set_build_mode(pbf_filter_t* f, int mode) {
+    if (!f) return fail(PBF_ERR_INVALID, "null filter handle");
+    if (mode < PBF_BUILD_AUTO || mode > PBF_BUILD_TILED) return fail(PBF_ERR_INVALID, "bad build mode");
+    if (mode == PBF_BUILD_TILED && !f->tiled_ok) return fail(PBF_ERR_INVALID, "tiled build unsupported for this m");
+    f->mode = mode;
+    return PBF_OK;
+}
+
+int pbf_last_build_mode(pbf_filter_t* f) { return f ? f->last_mode : 0; }
+
+int pbf_gen_splitmix_hex(int device, void* stream, uint8_t* out_dev, uint64_t seed, uint64_t start, uint64_t n) {
+    HIP_TRY(hipSetDevice(device));
+    if (n == 0) return PBF_OK;
+    if (!out_dev || (reinterpret_cast<uintptr_t>(out_dev) & 15)) return fail(PBF_ERR_INVALID, "out must be 16-B aligned");
+    k_gen_splitmix_hex<<<grid_for(n, 256), 256, 0, static_cast<hipStream_t>(stream)>>>(out_dev, seed, start, n);
+    CHECK_LAUNCH();
+    return PBF_OK;
+}
+
+int pbf_gen_varlen(int device, void* stream, uint8_t* out_dev, const uint64_t* offsets_dev, uint64_t seed,
+                   uint64_t start, uint64_t n) {
+    HIP_TRY(hipSetDevice(device));
+    if (n == 0) return PBF_OK;
+    if (!out_dev || !offsets_dev) return fail(PBF_ERR_INVALID, "null pointer");
+    k_gen_varlen<<<grid_for(n, 256), 256, 0, static_cast<hipStream_t>(stream)>>>(out_dev, offsets_dev, seed, start, n);
+    CHECK_LAUNCH();
+    return PBF_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,97 @@
+"""Device-resident path (keys and hit masks in HBM, torch as the allocator) and full-size
+properties at BASELINE.json's config-2 scale.  Runs on an MI355X (`-m gpu`)."""
+import numpy as np
+import pytest
+
+from pebbledb_amd import BloomFilter, PackedKeys
+from pebbledb_amd import _native
+from pebbledb_amd._native import PBF_BUILD_ATOMIC, PBF_BUILD_TILED
+from pebbledb_amd.keys import splitmix_hex_keys, varlen_keys
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+
+def dev_keys_hex(seed, start, n):
+    t = torch.empty(n * 16, dtype=torch.uint8, device="cuda")
+    _native.check(_native.lib().pbf_gen_splitmix_hex(0, None, t.data_ptr(), seed, start, n), "gen")
+    torch.cuda.synchronize()
+    return t
+
+
+def test_device_keygen_matches_numpy():
+    t = dev_keys_hex(0x5EEDB100, 12345, 5000)
+    assert np.array_equal(t.cpu().numpy().reshape(-1, 16), splitmix_hex_keys(0x5EEDB100, 12345, 5000))
+    d, o = varlen_keys(0xC3, 777, 3000)
+    od = torch.from_numpy(o.view(np.int64)).cuda()
+    out = torch.empty(int(o[-1]), dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    _native.check(_native.lib().pbf_gen_varlen(0, None, out.data_ptr(), od.data_ptr(), 0xC3, 777, 3000), "gen")
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), d)
+
+
+@pytest.mark.parametrize("mode", [PBF_BUILD_ATOMIC, PBF_BUILD_TILED])
+def test_device_resident_equals_host_path(oracle, mode):
+    n = 200000
+    keys = dev_keys_hex(9, 0, n)
+    host = PackedKeys.fixed(splitmix_hex_keys(9, 0, n))
+    bf = BloomFilter(2 ** 18, 6)
+    bf.set_build_mode(mode)
+    bf.add_device_fixed(keys.data_ptr(), 16, n)
+    q = dev_keys_hex(9, n // 2, n)
+    hm = torch.zeros((n + 7) // 8, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    bf.probe_device_fixed(q.data_ptr(), 16, n, hm.data_ptr())
+    bf.sync()
+    want = oracle.build(2 ** 18, 6, host)
+    assert bf.bitmap() == want.tobytes()
+    qh = PackedKeys.fixed(splitmix_hex_keys(9, n // 2, n))
+    assert np.array_equal(hm.cpu().numpy(), oracle.probe(want, 6, qh))
+    # variable-length on device, offsets not starting at 0 (a slice of a larger batch)
+    d, o = varlen_keys(21, 0, 30001)
+    od = torch.from_numpy(o.view(np.int64)).cuda()
+    dd = torch.from_numpy(d).cuda()
+    torch.cuda.synchronize()
+    sl = 1000  # keys [1000, 30001): offsets pointer shifted, data pointer at offsets[1000]
+    bfv = BloomFilter(40000, 7)
+    bfv.set_build_mode(mode)
+    bfv.add_device(dd.data_ptr() + int(o[sl]), od.data_ptr() + 8 * sl, 30001 - sl)
+    bfv.sync()
+    sub = PackedKeys(d[int(o[sl]):], 30001 - sl, offsets=o[sl:] - o[sl])
+    assert bfv.bitmap() == oracle.build(40000, 7, sub).tobytes()
+
+
+def test_config2_full_size_properties(oracle):
+    """C2: 10M 16-B keys, m = 2^30 (128 MiB), k = 6 — bit-exact vs the OpenMP oracle,
+    atomic == tiled, no false negatives, FPR at the theoretical value."""
+    n, nb, k = 10_000_000, 2 ** 27, 6
+    keys = dev_keys_hex(0x5EEDB100, 0, n)
+    a = BloomFilter(nb, k)
+    a.set_build_mode(PBF_BUILD_TILED)
+    a.add_device_fixed(keys.data_ptr(), 16, n)
+    b = BloomFilter(nb, k)
+    b.set_build_mode(PBF_BUILD_ATOMIC)
+    b.add_device_fixed(keys.data_ptr(), 16, n)
+    a.sync()
+    b.sync()
+    ba, bb = a.bitmap(), b.bitmap()
+    assert ba == bb
+    host = PackedKeys.fixed(keys.cpu().numpy().reshape(-1, 16))
+    want = oracle.build(nb, k, host, omp=True)
+    assert ba == want.tobytes()
+    # probes: n members + n non-members
+    q = dev_keys_hex(0x5EEDB100, 0, 2 * n)
+    hm = torch.zeros(2 * n // 8, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    a.probe_device_fixed(q.data_ptr(), 16, 2 * n, hm.data_ptr())
+    a.sync()
+    h = hm.cpu().numpy()
+    assert (h[: n // 8] == 0xFF).all()  # no false negatives
+    fp = int(np.unpackbits(h[n // 8:]).sum())
+    fill = a.popcount() / (8 * nb)
+    expect = n * fill ** k
+    assert fp <= 3 * expect + 20, (fp, expect)
+    # the non-member hit mask equals the oracle's on a 1M sample
+    qs = PackedKeys.fixed(splitmix_hex_keys(0x5EEDB100, n, 1_000_000))
+    assert np.array_equal(h[n // 8: n // 8 + 125000], oracle.probe(want, k, qs, omp=True))

@@ -1,0 +1,300 @@
+"""GPU parity: the HIP path (through the C-ABI) against the oracle and the reference's golden
+vectors.  Bit-exact for every bitmap, hit mask and index.  Runs on an MI355X (`-m gpu`)."""
+import hashlib
+
+import numpy as np
+import pytest
+
+from conftest import load_golden
+from pebbledb_amd import BloomFilter, PackedKeys
+from pebbledb_amd._native import PBF_BUILD_ATOMIC, PBF_BUILD_AUTO, PBF_BUILD_TILED
+from pebbledb_amd.keys import splitmix_hex_keys, varlen_keys
+
+pytestmark = pytest.mark.gpu
+
+MODES = [PBF_BUILD_ATOMIC, PBF_BUILD_TILED]
+
+
+def built(nb, k, keys, mode=PBF_BUILD_AUTO):
+    bf = BloomFilter(nb, k)
+    if mode != PBF_BUILD_AUTO:
+        bf.set_build_mode(mode)
+    bf.add_many(keys)
+    return bf
+
+
+def bits_of(hm, n):
+    return [bool(hm[i >> 3] >> (i & 7) & 1) for i in range(n)]
+
+
+# ---------------------------------------------------------------- the reference's own tests
+def test_reference_test_lookups():
+    # src/__tests__/test_bloom_filter.py:4-20
+    bf = BloomFilter(nb_bytes=4, nb_hash_functions=3)
+    for key in ["foo", "bar", "baz"]:
+        bf.add(key=key)
+    for key in ["foo", "bar", "baz"]:
+        assert bf.may_contain(key=key) is True
+    for key in ["not_in_bloom_filter", "missing"]:
+        assert bf.may_contain(key=key) is False
+
+
+def test_reference_build_from_keys():
+    bf = BloomFilter.build_from_keys_and_fp_rate(["key1", "key2"], 0.001)
+    assert bf.may_contain("key1") is True and bf.may_contain("key2") is True
+
+
+@pytest.mark.parametrize("nb,expected", [(1, b"3"), (3, b"\x003\x10")])
+def test_reference_encode(nb, expected):
+    # test_bloom_filter.py:32-61
+    bf = BloomFilter(nb_bytes=nb, nb_hash_functions=2)
+    for key in ["key1", "key2", "key3"]:
+        bf.add(key)
+    assert bf.to_bytes() == expected + b"\x02"
+    assert BloomFilter.from_bytes(bf.to_bytes()) == bf  # :64-91
+
+
+def test_reference_equality():
+    # test_bloom_filter.py:94-140
+    keys = ["key1", "key2", "key3"]
+    a, b = BloomFilter(8, 3), BloomFilter(8, 3)
+    c = BloomFilter(8, 4)
+    for key in keys:
+        a.add(key)
+        b.add(key)
+        c.add(key)
+    assert (a == b) is True
+    assert (a == c) is False
+    d = BloomFilter(8, 4)
+    for key in keys[:2]:
+        d.add(key)
+    assert (a == d) is False
+    # __eq__ ignores nb_bytes (bloom_filter.py:36)
+    e = BloomFilter(16, 3, bits=a.bits)
+    assert e == a
+
+
+def test_reference_lsm_negative():
+    # test_lsm_storage.py:287-317: m=16, k=3, "baz" must be a negative
+    bf = BloomFilter(nb_bytes=2, nb_hash_functions=3)
+    for key in ["foo", "bar"]:
+        bf.add(key=key)
+    assert bf.may_contain("foo") and bf.may_contain("bar")
+    assert bf.may_contain("baz") is False
+
+
+def test_golden_kats_all():
+    for c in load_golden("reference_kats.json")["cases"]:
+        bf = BloomFilter(c["nb_bytes"], c["k"])
+        for key in c["keys"]:
+            bf.add(key)
+        assert bf.to_bytes().hex() == c["to_bytes_hex"]
+        assert bf.bits == int(c["bits"])
+        assert [bf.may_contain(p) for p in c["probes"]] == c["probe_results"]
+
+
+# ---------------------------------------------------------------- index math (any m)
+def test_index_math_golden():
+    for c in load_golden("index_math.json")["cases"]:
+        bf = BloomFilter(c["nb_bytes"], c["k"])
+        for key, want in zip(c["keys"], c["indices"]):
+            assert bf._hash(key) == want, (c["nb_bytes"], key)
+        del bf
+
+
+def test_large_m_set_bits_both_modes():
+    for c in load_golden("large_m.json")["cases"]:
+        keys = [f"{i:016d}" for i in range(64)]
+        for mode in MODES:
+            bf = built(c["nb_bytes"], c["k"], keys, mode)
+            bm = np.frombuffer(bf.bitmap(), dtype=np.uint8)
+            bits = np.unpackbits(bm, bitorder="little")
+            got = np.flatnonzero(bits).tolist()
+            assert got == c["set_bits"], (c["nb_bytes"], mode)
+            del bf, bm, bits
+
+
+# ---------------------------------------------------------------- golden bitmaps
+def _check_desc(bf, d):
+    b = bf.bitmap()
+    assert hashlib.sha256(b).hexdigest() == d["sha256"]
+    assert bf.popcount() == d["popcount"]
+    if "to_bytes_hex" in d:
+        assert bf.to_bytes().hex() == d["to_bytes_hex"]
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_config1_golden(mode):
+    g = load_golden("config1.json")
+    keys = [f"{i:016d}" for i in range(1000)]
+    bf = built(1024, 4, keys, mode)
+    _check_desc(bf, g["config1"])
+    hm = bf.may_contain_many([f"{i:016d}" for i in range(11000)], packed=True)
+    assert hm.tobytes().hex() == g["config1"]["probe_hitmask_hex"]
+    bfp = BloomFilter.build_from_keys_and_fp_rate(keys, 0.001)
+    _check_desc(bfp, g["product_p0001"])
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_splitmix_golden(mode):
+    g = load_golden("splitmix16.json")
+    members = PackedKeys.fixed(splitmix_hex_keys(g["seed"], 0, g["members"]))
+    non = PackedKeys.fixed(splitmix_hex_keys(g["seed"], g["nonmember_start"], g["nonmembers"]))
+    bf = built(8192, 6, members, mode)
+    _check_desc(bf, g["pow2"])
+    assert bf.may_contain_many(non, packed=True).tobytes().hex() == g["pow2"]["hitmask_nonmembers_hex"]
+    bf2 = built(6007, 7, PackedKeys.fixed(splitmix_hex_keys(g["seed"], 0, 5000)), mode)
+    _check_desc(bf2, g["odd"])
+    assert bf2.may_contain_many(non, packed=True).tobytes().hex() == g["odd"]["hitmask_nonmembers_hex"]
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_varlen_and_unicode_golden(mode):
+    g = load_golden("varlen.json")
+    d, o = varlen_keys(g["seed"], 0, g["members"])
+    bf = built(8192, 8, PackedKeys(d, g["members"], offsets=o), mode)
+    _check_desc(bf, g["varlen"])
+    d2, o2 = varlen_keys(g["seed"], g["nonmember_start"], g["nonmembers"])
+    hm = bf.may_contain_many(PackedKeys(d2, g["nonmembers"], offsets=o2), packed=True)
+    assert hm.tobytes().hex() == g["varlen"]["hitmask_nonmembers_hex"]
+    sk = [(f"{i:08d}" * 8)[:8 + i % 57] for i in range(1000)]
+    _check_desc(built(1024, 8, sk, mode), g["survey_family"])
+    u = load_golden("unicode.json")
+    bfu = built(u["nb_bytes"], u["nb_hash_functions"], u["keys"], mode)
+    _check_desc(bfu, u)
+    hm = bfu.may_contain_many(u["keys"] + [f"absent-{i}" for i in range(200)], packed=True)
+    assert hm.tobytes().hex() == u["hitmask_hex"]
+
+
+# ---------------------------------------------------------------- oracle sweeps
+CASES = [
+    # (nb_bytes, k, key kind, n)
+    (1, 1, "hex16", 100), (3, 2, "hex16", 50), (1000, 3, "hex16", 3000), (6007, 7, "var", 4000),
+    (123457, 6, "hex16", 200000), (2 ** 20 + 3, 10, "hex16", 300000), (2 ** 20, 8, "var", 100000),
+    (77777, 17, "hex16", 20000), (5000, 33, "var", 3000), (4096, 40, "fixed7", 2000),
+    (2 ** 24, 6, "fixed7", 500000), (2 ** 27, 6, "hex16", 1000000), (17971985, 10, "hex16", 1000000),
+]
+
+
+def make_keys(kind, n, start=0):
+    if kind == "hex16":
+        return PackedKeys.fixed(splitmix_hex_keys(11, start, n))
+    if kind == "fixed7":
+        return PackedKeys.fixed(splitmix_hex_keys(13, start, n)[:, 3:10])
+    d, o = varlen_keys(17, start, n)
+    return PackedKeys(d, n, offsets=o)
+
+
+@pytest.mark.parametrize("nb,k,kind,n", CASES)
+def test_sweep_against_oracle(oracle, nb, k, kind, n):
+    keys = make_keys(kind, n)
+    want = oracle.build(nb, k, keys, omp=True)
+    probes = make_keys(kind, n // 2 + 7, start=n - n // 4)
+    want_hm = oracle.probe(want, k, probes, omp=True)
+    for mode in MODES:
+        bf = built(nb, k, keys, mode)
+        got = np.frombuffer(bf.bitmap(), dtype=np.uint8)
+        assert np.array_equal(got, want), (mode, int((got != want).sum()))
+        assert np.array_equal(bf.may_contain_many(probes, packed=True), want_hm)
+        del bf
+
+
+def test_unaligned_and_odd_lengths(oracle):
+    raw = splitmix_hex_keys(5, 0, 5001)
+    buf = np.zeros(raw.size + 1, dtype=np.uint8)
+    buf[1:] = raw.reshape(-1)
+    pk = PackedKeys(buf[1:], 5001, key_len=16)  # 16-byte keys at an odd address → generic path
+    assert pk.data.ctypes.data % 16 != 0
+    want = oracle.build(3001, 5, pk)
+    for mode in MODES:
+        assert np.array_equal(np.frombuffer(built(3001, 5, pk, mode).bitmap(), np.uint8), want)
+    for L in (1, 2, 3, 4, 5, 9, 15, 31, 33, 63, 64, 65, 200):
+        keys = [("x" * L + str(i))[:L] if L else "" for i in range(300)]
+        pk = PackedKeys.from_strs(keys)
+        want = oracle.build(999, 4, pk)
+        for mode in MODES:
+            assert np.array_equal(np.frombuffer(built(999, 4, pk, mode).bitmap(), np.uint8), want), L
+
+
+def test_empty_keys_and_empty_batches(oracle):
+    keys = ["", "", "a", ""]
+    pk = PackedKeys.from_strs(keys)
+    want = oracle.build(64, 5, pk)
+    bf = BloomFilter(64, 5)
+    bf.add_many(keys)
+    assert bf.bitmap() == want.tobytes()
+    assert bf.may_contain("") is True
+    only_empty = BloomFilter(64, 5)
+    only_empty.add_many(["", ""])
+    assert only_empty.bitmap() == oracle.build(64, 5, PackedKeys.from_strs([""])).tobytes()
+    bf.add_many([])
+    assert bf.may_contain_many([]).size == 0
+    with pytest.raises(ZeroDivisionError):
+        BloomFilter.build_from_keys_and_fp_rate([], 0.001)
+    z = BloomFilter(0, 3)
+    with pytest.raises(ZeroDivisionError):
+        z.add("a")
+    assert BloomFilter(0, 0).may_contain("x") is True  # no hash function → vacuous AND
+    assert BloomFilter(8, 0).may_contain("x") is True
+    with pytest.raises(Exception):  # struct.error, as bloom_filter.py:80
+        BloomFilter(8, 300).to_bytes()
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_incremental_batches(oracle, mode):
+    keys = make_keys("hex16", 300000)
+    want = oracle.build(2 ** 20, 6, keys, omp=True)
+    bf = BloomFilter(2 ** 20, 6)
+    bf.set_build_mode(mode)
+    for s in range(0, 300000, 70001):
+        e = min(300000, s + 70001)
+        bf.add_many(PackedKeys.fixed(keys.data.reshape(-1, 16)[s:e]))
+    assert np.array_equal(np.frombuffer(bf.bitmap(), np.uint8), want)
+    # from_bytes then more adds (non-pristine tiled path)
+    half = PackedKeys.fixed(keys.data.reshape(-1, 16)[:150000])
+    rest = PackedKeys.fixed(keys.data.reshape(-1, 16)[150000:])
+    bf2 = BloomFilter.from_bytes(built(2 ** 20, 6, half).to_bytes())
+    bf2.set_build_mode(mode)
+    bf2.add_many(rest)
+    assert np.array_equal(np.frombuffer(bf2.bitmap(), np.uint8), want)
+    bf2.clear()
+    assert bf2.popcount() == 0
+    bf2.add_many(keys)
+    assert np.array_equal(np.frombuffer(bf2.bitmap(), np.uint8), want)
+
+
+def test_hitmask_tails(oracle):
+    keys = make_keys("hex16", 1000)
+    want = oracle.build(4096, 6, keys)
+    bf = built(4096, 6, keys)
+    for n in (1, 7, 8, 9, 63, 64, 65, 127, 129, 1000):
+        q = PackedKeys.fixed(keys.data.reshape(-1, 16)[:n])
+        assert np.array_equal(bf.may_contain_many(q, packed=True), oracle.probe(want, 6, q)), n
+        assert bf.may_contain_many(q).all()
+
+
+def test_small_host_stage_chunks(oracle, monkeypatch):
+    """The host→device chunking path (PBF_STAGE_BYTES) in a child process."""
+    import subprocess, sys, os, textwrap
+    code = textwrap.dedent("""
+        import numpy as np, sys
+        sys.path.insert(0, '.')
+        from pebbledb_amd import BloomFilter, PackedKeys
+        from pebbledb_amd.keys import splitmix_hex_keys, varlen_keys
+        from oracle.oracle import COracle
+        o = COracle()
+        fx = PackedKeys.fixed(splitmix_hex_keys(3, 0, 20000))
+        d, off = varlen_keys(3, 0, 20000)
+        vr = PackedKeys(d, 20000, offsets=off)
+        for pk in (fx, vr):
+            for mode in (1, 2):
+                bf = BloomFilter(50000, 6); bf.set_build_mode(mode); bf.add_many(pk)
+                want = o.build(50000, 6, pk)
+                assert bf.bitmap() == want.tobytes()
+                assert np.array_equal(bf.may_contain_many(pk, packed=True), o.probe(want, 6, pk))
+        print('ok')
+    """)
+    env = dict(os.environ, PBF_STAGE_BYTES="4099")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=600,
+                       cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]

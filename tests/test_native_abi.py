@@ -1,0 +1,52 @@
+"""CPU-side checks of the C-ABI library: it loads and exports every symbol the header declares.
+
+No compute calls here (there is no GPU in the build container)."""
+import ctypes
+import os
+import subprocess
+
+import pytest
+
+from pebbledb_amd import _native
+
+
+def test_header_declares_expected_functions():
+    names = _native.header_functions()
+    assert "pbf_create" in names and "pbf_probe" in names and "pbf_add" in names
+    assert set(names) == set(_native.SIGNATURES), set(names) ^ set(_native.SIGNATURES)
+
+
+def test_library_loads_and_exports_every_header_symbol():
+    L = _native.lib()
+    for name in _native.header_functions():
+        assert hasattr(L, name), name
+    out = subprocess.run(["nm", "-D", "--defined-only", _native.LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    exported = {line.split()[-1] for line in out.splitlines() if " T " in line}
+    assert set(_native.header_functions()) <= exported
+
+
+def test_library_targets_gfx950_only():
+    data = open(_native.LIB_PATH, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in data
+    assert b"gfx942" not in data and b"gfx90a" not in data
+
+
+def test_version_and_error_string_without_gpu():
+    L = _native.lib()
+    assert L.pbf_version() >= 100
+    assert isinstance(L.pbf_last_error(), bytes)
+    # argument validation happens before any device call
+    h = ctypes.c_void_p()
+    assert L.pbf_create(0, 0, 3, ctypes.byref(h)) == _native.PBF_ERR_ZERO_SIZE
+    assert b"modulo by zero" in L.pbf_last_error()
+    assert L.pbf_sync(None) == _native.PBF_ERR_INVALID
+
+
+def test_product_package_never_imports_the_oracle():
+    pkg = os.path.dirname(_native.__file__)
+    for root, _, files in os.walk(pkg):
+        for f in files:
+            if f.endswith((".py", ".hip", ".hpp", ".h", ".cpp")):
+                text = open(os.path.join(root, f)).read()
+                assert "oracle" not in text.replace("oracle/", "").lower() or f == "__init__.py", f
