@@ -41,7 +41,10 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--build-mode", type=int, default=0, help="0 auto, 1 atomic, 2 tiled")
+    ap.add_argument("--probe-mode", type=int, default=0, help="0 auto, 1 direct, 2 tiled")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-events", action="store_true", help="diagnostic: time without per-step HIP events")
+    ap.add_argument("--sync-each-step", action="store_true", help="diagnostic: synchronise after every step")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the bounded CPU sample")
     return ap.parse_args()
 
@@ -156,6 +159,8 @@ def main():
     bf = BloomFilter(nb_bytes, k, device=local)
     if args.build_mode:
         bf.set_build_mode(args.build_mode)
+    if args.probe_mode:
+        bf.set_probe_mode(args.probe_mode)
     stream = torch.cuda.ExternalStream(bf.stream)
 
     def step(ev=None):
@@ -190,15 +195,23 @@ def main():
     bf.sync()
     t0 = time.perf_counter()
     for s in range(args.steps):
-        step(events[s])
+        step(None if args.no_events else events[s])
+        if args.sync_each_step:
+            bf.sync()
+    t_enq = time.perf_counter()
     bf.sync()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     if world > 1:
         dist.barrier()
     elapsed = t1 - t0
-    build_ms = sum(e[0].elapsed_time(e[1]) for e in events) / args.steps
-    probe_ms = sum(e[1].elapsed_time(e[2]) for e in events) / args.steps
+    if args.no_events:
+        for s in range(min(args.steps, 5)):  # time a few steps separately for the roofline
+            step(events[s])
+        bf.sync()
+        events = events[:min(args.steps, 5)]
+    build_ms = sum(e[0].elapsed_time(e[1]) for e in events) / len(events)
+    probe_ms = sum(e[1].elapsed_time(e[2]) for e in events) / len(events)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -218,10 +231,11 @@ def main():
         ach_probe = b_probe / (probe_ms * 1e-3) / 1e9
         if build_ms >= probe_ms:
             dom = {"kernel": f"build pass ({'tiled' if bf.last_build_mode == 2 else 'atomic'}: "
-                             f"{'k_hist+k_colscan+k_basescan+k_scatter+k_tile' if bf.last_build_mode == 2 else 'k_build_atomic'})",
+                             f"{'k_part+k_tile_build+k_ovf_build' if bf.last_build_mode == 2 else 'k_build_atomic'})",
                    "achieved": ach_build, "ms": build_ms, "bytes": b_build}
         else:
-            dom = {"kernel": "k_probe", "achieved": ach_probe, "ms": probe_ms, "bytes": b_probe}
+            dom = {"kernel": ("probe pass (tiled: k_part<probe>+k_tile_probe+k_gather)" if bf.last_probe_mode == 2
+                              else "k_probe"), "achieved": ach_probe, "ms": probe_ms, "bytes": b_probe}
         out = {
             "metric": "Mkeys/s bloom build+probe (device-resident), 10M 16B keys; 1/2/4/8 GPU",
             "value": round(value, 3),
@@ -239,11 +253,13 @@ def main():
                                    f" bits (nb_bytes={nb_bytes}), k={k}; probe {2 * n} keys ({n} members + {n} absent)"
                                    f"; one filter per GPU", "n_build": n, "n_probe": 2 * n, "nb_bytes": nb_bytes, "k": k,
                        "keys_per_step_per_gpu": 3 * n, "parallelism": f"filter-per-gpu x{world}"},
+            "host_enqueue_ms_per_step": round((t_enq - t0) / args.steps * 1e3, 4),
             "build_ms": round(build_ms, 4),
             "probe_ms": round(probe_ms, 4),
             "build_Mkeys_s_per_gpu": round(n / build_ms / 1e3, 1),
             "probe_Mkeys_s_per_gpu": round(2 * n / probe_ms / 1e3, 1),
             "build_mode": bf.last_build_mode,
+            "probe_mode": bf.last_probe_mode,
             "roofline": {"bound": "hbm", "achieved": round(dom["achieved"], 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(dom["achieved"] / HBM_PEAK_GBS, 4), "traffic": None, "kernel": dom["kernel"],
                          "algorithmic_bytes": int(dom["bytes"]), "avg_ms": round(dom["ms"], 4)},

@@ -43,6 +43,11 @@ extern "C" {
 #define PBF_BUILD_ATOMIC 1 /* one lane per key, k global atomicOr */
 #define PBF_BUILD_TILED 2  /* partition positions by LDS tile, OR in LDS, write tiles once */
 
+/* Probe strategies (pbf_set_probe_mode).  All give identical hit masks. */
+#define PBF_PROBE_AUTO 0
+#define PBF_PROBE_DIRECT 1 /* one lane per key, k random word loads, wave ballot */
+#define PBF_PROBE_TILED 2  /* partition (key, position) entries by LDS tile, test in LDS, gather */
+
 typedef struct pbf_filter pbf_filter_t;
 
 /* Library version (major*10000 + minor*100 + patch). */
@@ -103,6 +108,11 @@ void* pbf_device_bitmap(pbf_filter_t* f);
  * returned by pbf_last_build_mode. */
 int pbf_set_build_mode(pbf_filter_t* f, int mode);
 int pbf_last_build_mode(pbf_filter_t* f);
+
+/* Select the probe strategy (PBF_PROBE_*); the one used by the last probe is returned by
+ * pbf_last_probe_mode. */
+int pbf_set_probe_mode(pbf_filter_t* f, int mode);
+int pbf_last_probe_mode(pbf_filter_t* f);
 
 /* Synthetic keys straight into device memory (bench / tests; definitions in
  * pebbledb_amd/keys.py): 16 hex chars of splitmix64(seed + start + i), and the variable-length

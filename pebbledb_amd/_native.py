@@ -17,6 +17,7 @@ PBF_ERR_INVALID = -1
 PBF_ERR_HIP = -2
 PBF_ERR_ZERO_SIZE = -3
 PBF_BUILD_AUTO, PBF_BUILD_ATOMIC, PBF_BUILD_TILED = 0, 1, 2
+PBF_PROBE_AUTO, PBF_PROBE_DIRECT, PBF_PROBE_TILED = 0, 1, 2
 
 _u8p = ctypes.c_void_p
 _vp = ctypes.c_void_p
@@ -45,6 +46,8 @@ SIGNATURES = {
     "pbf_device_bitmap": (_vp, [_vp]),
     "pbf_set_build_mode": (_int, [_vp, _int]),
     "pbf_last_build_mode": (_int, [_vp]),
+    "pbf_set_probe_mode": (_int, [_vp, _int]),
+    "pbf_last_probe_mode": (_int, [_vp]),
     "pbf_gen_splitmix_hex": (_int, [_int, _vp, _u8p, _u64, _u64, _u64]),
     "pbf_gen_varlen": (_int, [_int, _vp, _u8p, _vp, _u64, _u64, _u64]),
     "pbf_last_error": (ctypes.c_char_p, []),

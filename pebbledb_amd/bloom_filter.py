@@ -270,6 +270,14 @@ class BloomFilter:
         if self._h is not None:
             _native.check(_native.lib().pbf_set_build_mode(self._h, int(mode)), "pbf_set_build_mode")
 
+    def set_probe_mode(self, mode: int) -> None:
+        if self._h is not None:
+            _native.check(_native.lib().pbf_set_probe_mode(self._h, int(mode)), "pbf_set_probe_mode")
+
+    @property
+    def last_probe_mode(self) -> int:
+        return 0 if self._h is None else _native.lib().pbf_last_probe_mode(self._h)
+
     @property
     def last_build_mode(self) -> int:
         return 0 if self._h is None else _native.lib().pbf_last_build_mode(self._h)

@@ -11,14 +11,18 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <string>
 #include <type_traits>
 
 #include "../../include/pebblebloom.h"
 #include "bloom_kernels.hpp"
+#include "tiled_kernels.hpp"
 
 using namespace pbf;
 
@@ -92,6 +96,16 @@ size_t stage_bytes() {
 }
 constexpr uint64_t kMaxPositions = uint64_t(1) << 30; // tiled pipeline batch (4 GiB of positions)
 
+// Words loaded in the probe's first stage (PBF_PROBE_S1 overrides; tuning knob).
+int probe_stage1() {
+    static const int v = [] {
+        const char* e = std::getenv("PBF_PROBE_S1");
+        const int x = e ? std::atoi(e) : 0;
+        return x > 0 ? x : 2;
+    }();
+    return v;
+}
+
 int kmax_for(uint32_t k) {
     if (k <= 4) return 4;
     if (k <= 8) return 8;
@@ -134,12 +148,24 @@ IndexMap make_index_map(uint64_t m) {
     return im;
 }
 
-// Dynamic LDS above 64 KiB must be allowed per kernel (gfx950 has 160 KiB per CU).
+// Dynamic LDS above 64 KiB must be allowed per kernel (gfx950 has 160 KiB per CU).  The
+// attribute call is slow (~0.5 ms): do it once per (device, kernel) at the largest size seen.
 template <class K>
 hipError_t allow_lds(K kernel, size_t bytes) {
     if (bytes <= 65536) return hipSuccess;
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
-                               int(bytes));
+    static std::mutex mu;
+    static std::map<std::pair<int, const void*>, size_t> done;
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    const auto key = std::make_pair(dev, reinterpret_cast<const void*>(kernel));
+    std::lock_guard<std::mutex> lock(mu);
+    auto it = done.find(key);
+    if (it != done.end() && it->second >= bytes) return hipSuccess;
+    e = hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            int(bytes));
+    if (e == hipSuccess) done[key] = bytes;
+    return e;
 }
 
 uint32_t ceil_log2(uint64_t x) {
@@ -165,7 +191,9 @@ struct pbf_filter {
     IndexMap im{};
     TileMap tm{};
     bool tiled_ok = false;
-    DevBuf positions, counts, total, base;
+    int probe_mode = PBF_PROBE_AUTO;
+    int last_probe_mode = 0;
+    DevBuf regions, fill, ovf, ovf_count, subcnt, rbits, neg;
     DevBuf dkeys, doffs, dout;
     PinBuf pin[2];
     int pin_next = 0;
@@ -227,70 +255,114 @@ int run_atomic(pbf_filter_t* f, const Batch& b) {
     return PBF_OK;
 }
 
-// Scatter-kernel geometry for B tiles: (workgroups, keys per sub-chunk, LDS bytes).
-void scatter_geometry(uint32_t B, uint32_t k, uint64_t n, uint32_t* G, uint32_t* keys_per_sub, size_t* lds) {
+// Geometry of the partition pass for a batch of n keys (see tiled_kernels.hpp).
+struct PartPlan {
+    PartGeom pg;
+    size_t lds_part;
+};
+
+PartPlan plan_partition(uint32_t B, uint32_t k, int km, uint64_t n, bool probe) {
+    PartPlan pl{};
     const size_t fixed = size_t(3 * B + 1 + 16) * 4;
-    // Two workgroups per CU (<= 78 KiB each) while that leaves >= 12K staged positions,
-    // otherwise one (<= 156 KiB).
-    size_t budget = 78 * 1024;
-    uint32_t per_cu = 2;
-    if (budget < fixed + 12288 * 4) {
-        budget = 156 * 1024;
-        per_cu = 1;
-    }
-    const uint64_t stage = (budget - fixed) / 4;
-    const uint32_t kps = uint32_t(std::max<uint64_t>(1, stage / k));
-    *keys_per_sub = kps;
-    *lds = fixed + size_t(kps) * k * 4;
-    const uint64_t want = 256ull * per_cu;
-    const uint64_t by_n = std::max<uint64_t>(1, (n + 2047) / 2048);
-    *G = uint32_t(std::min(want, by_n));
+    // keys per thread per sub-chunk: as many as the registers (part_kpt) and 156 KiB of LDS allow
+    uint64_t kpt = uint64_t(part_kpt(kmax_for(k), km, probe));
+    while (kpt > 1 && fixed + kpt * kPartThreads * k * 4 > 156 * 1024) --kpt;
+    if (probe) kpt = std::min<uint64_t>(kpt, (kSlotMask + 1) / kPartThreads);
+    const uint64_t kps = kpt * kPartThreads;
+    pl.lds_part = fixed + size_t(kps) * k * 4;
+    const uint64_t G0 = std::min<uint64_t>(256, std::max<uint64_t>(1, (n + kps - 1) / kps));
+    uint64_t kpw = (n + G0 - 1) / G0;
+    kpw = ((kpw + kps - 1) / kps) * kps;
+    pl.pg.G = uint32_t(std::max<uint64_t>(1, (n + kpw - 1) / kpw));
+    pl.pg.kps = uint32_t(kps);
+    pl.pg.kpw = kpw;
+    pl.pg.nsub = uint32_t(kpw / kps);
+    const double mu = double(kpw) * k / B;
+    const uint64_t cap = uint64_t(mu + 8.0 * std::sqrt(mu) + 32.0);
+    pl.pg.cap = uint32_t(((cap + 31) / 32) * 32);
+    return pl;
 }
 
 int run_tiled(pbf_filter_t* f, const Batch& b) {
     const TileMap& tm = f->tm;
     const uint32_t B = tm.nbuckets;
     const uint32_t k = f->k;
-    uint32_t G, kps;
-    size_t lds_scatter;
-    scatter_geometry(B, k, b.n, &G, &kps, &lds_scatter);
-    const uint64_t kpw = (b.n + G - 1) / G;
-    const uint64_t npos = b.n * k;
-    HIP_TRY(f->positions.ensure(std::max<uint64_t>(npos, 1) * 4));
-    HIP_TRY(f->counts.ensure(size_t(G) * B * 4));
-    HIP_TRY(f->total.ensure(size_t(B) * 4));
-    HIP_TRY(f->base.ensure(size_t(B + 1) * 4));
-    auto* counts = static_cast<uint32_t*>(f->counts.p);
-    auto* total = static_cast<uint32_t*>(f->total.p);
-    auto* base = static_cast<uint32_t*>(f->base.p);
-    auto* pos = static_cast<uint32_t*>(f->positions.p);
+    const PartPlan pl = plan_partition(B, k, b.km, b.n, false);
+    const PartGeom& pg = pl.pg;
+    HIP_TRY(f->regions.ensure(size_t(pg.G) * B * pg.cap * 4));
+    HIP_TRY(f->fill.ensure(size_t(pg.G) * B * 4));
+    HIP_TRY(f->ovf.ensure(std::max<uint64_t>(b.n * k, 1) * 4));
+    HIP_TRY(f->ovf_count.ensure(64));
+    auto* regions = static_cast<uint32_t*>(f->regions.p);
+    auto* fill = static_cast<uint32_t*>(f->fill.p);
+    auto* ovf = static_cast<uint32_t*>(f->ovf.p);
+    auto* ovf_count = static_cast<uint32_t*>(f->ovf_count.p);
     hipStream_t s = f->stream;
+    HIP_TRY(hipMemsetAsync(ovf_count, 0, 4, s));
     hipError_t err = hipSuccess;
     dispatch(kmax_for(k), b.km, [&](auto KMAX, auto KM) {
-        auto kern = k_hist<decltype(KMAX)::value, decltype(KM)::value>;
-        err = allow_lds(kern, size_t(B) * 4);
-        if (err == hipSuccess) kern<<<G, 1024, size_t(B) * 4, s>>>(b.ks, b.n, int(k), tm, kpw, counts);
+        if constexpr (decltype(KMAX)::value > 0) {  // tiled path only for k <= 32
+            auto kern = k_part<decltype(KMAX)::value, decltype(KM)::value, false>;
+            err = allow_lds(kern, pl.lds_part);
+            if (err == hipSuccess)
+                kern<<<pg.G, kPartThreads, pl.lds_part, s>>>(b.ks, b.n, int(k), tm, pg, regions, fill, nullptr, ovf,
+                                                     ovf_count, nullptr, nullptr);
+        }
     });
     HIP_TRY(err);
     CHECK_LAUNCH();
-    k_colscan<<<(B + 63) / 64, 1024, 0, s>>>(counts, G, B, total);
+    const size_t lds_tile = ((size_t(1) << tm.tb) / 32 + pg.G) * 4;
+    HIP_TRY(allow_lds(k_tile_build, lds_tile));
+    k_tile_build<<<B, 1024, lds_tile, s>>>(tm, pg, regions, fill, f->bitmap, f->pristine ? 1 : 0);
     CHECK_LAUNCH();
-    const size_t lds_base = size_t(2 * B + 1 + 16) * 4;
-    HIP_TRY(allow_lds(k_basescan, lds_base));
-    k_basescan<<<1, 1024, lds_base, s>>>(total, B, base);
-    CHECK_LAUNCH();
-    dispatch(kmax_for(k), b.km, [&](auto KMAX, auto KM) {
-        auto kern = k_scatter<decltype(KMAX)::value, decltype(KM)::value>;
-        err = allow_lds(kern, lds_scatter);
-        if (err == hipSuccess) kern<<<G, 1024, lds_scatter, s>>>(b.ks, b.n, int(k), tm, kpw, kps, counts, base, pos);
-    });
-    HIP_TRY(err);
-    CHECK_LAUNCH();
-    const size_t lds_tile = (size_t(1) << tm.tb) / 8;
-    HIP_TRY(allow_lds(k_tile, lds_tile));
-    k_tile<<<B, 1024, lds_tile, s>>>(pos, base, tm, f->bitmap, f->pristine ? 1 : 0);
+    k_ovf_build<<<256, 256, 0, s>>>(tm, ovf, ovf_count, f->bitmap);
     CHECK_LAUNCH();
     f->pristine = false;
+    return PBF_OK;
+}
+
+int run_tiled_probe(pbf_filter_t* f, const Batch& b, uint8_t* hitmask) {
+    const TileMap& tm = f->tm;
+    const uint32_t B = tm.nbuckets;
+    const uint32_t k = f->k;
+    const PartPlan pl = plan_partition(B, k, b.km, b.n, true);
+    const PartGeom& pg = pl.pg;
+    HIP_TRY(f->regions.ensure(size_t(pg.G) * B * pg.cap * 4));
+    HIP_TRY(f->fill.ensure(size_t(pg.G) * B * 4));
+    HIP_TRY(f->subcnt.ensure(size_t(pg.G) * pg.nsub * B * 4));
+    HIP_TRY(f->rbits.ensure(size_t(pg.G) * B * (pg.cap / 32) * 4));
+    const size_t neg_bytes = ((b.n + 31) / 32) * 4;
+    HIP_TRY(f->neg.ensure(neg_bytes));
+    auto* regions = static_cast<uint32_t*>(f->regions.p);
+    auto* fill = static_cast<uint32_t*>(f->fill.p);
+    auto* subcnt = static_cast<uint32_t*>(f->subcnt.p);
+    auto* R = static_cast<uint32_t*>(f->rbits.p);
+    auto* neg = static_cast<uint32_t*>(f->neg.p);
+    hipStream_t s = f->stream;
+    HIP_TRY(hipMemsetAsync(neg, 0, neg_bytes, s));
+    hipError_t err = hipSuccess;
+    dispatch(kmax_for(k), b.km, [&](auto KMAX, auto KM) {
+        if constexpr (decltype(KMAX)::value > 0) {
+            auto kern = k_part<decltype(KMAX)::value, decltype(KM)::value, true>;
+            err = allow_lds(kern, pl.lds_part);
+            if (err == hipSuccess)
+                kern<<<pg.G, kPartThreads, pl.lds_part, s>>>(b.ks, b.n, int(k), tm, pg, regions, fill, subcnt, nullptr,
+                                                     nullptr, f->bitmap, neg);
+        }
+    });
+    HIP_TRY(err);
+    CHECK_LAUNCH();
+    size_t lds_tile = ((size_t(1) << tm.tb) / 32 + 2 * pg.G + 1 + 16) * 4;
+    const size_t lds_expand = size_t(pg.G) * (pg.cap / 32) * 2;
+    const int expand = lds_tile + lds_expand <= 160 * 1024 ? 1 : 0;
+    if (expand) lds_tile += lds_expand;
+    HIP_TRY(allow_lds(k_tile_probe, lds_tile));
+    k_tile_probe<<<B, 1024, lds_tile, s>>>(tm, pg, regions, fill, f->bitmap, R, expand);
+    CHECK_LAUNCH();
+    const size_t lds_gather = (size_t(2) * B + pg.kps) * 4;
+    HIP_TRY(allow_lds(k_gather, lds_gather));
+    k_gather<<<pg.G, 1024, lds_gather, s>>>(tm, pg, b.n, regions, R, subcnt, neg, hitmask);
+    CHECK_LAUNCH();
     return PBF_OK;
 }
 
@@ -299,10 +371,20 @@ bool want_tiled(pbf_filter_t* f, uint64_t n) {
     if (f->mode == PBF_BUILD_TILED) return true;
     if (f->mode == PBF_BUILD_ATOMIC) return false;
     const uint64_t npos = n * f->k;
-    // the tile pass streams the whole bitmap once (twice when not pristine); random atomics
-    // cost ~16x a streamed position.  Tiles win once positions are a small fraction of it.
+    // the tile pass streams the whole bitmap once (twice when not pristine); a random atomic
+    // costs ~16x a streamed position.  Tiles win once positions are a small fraction of it.
     const uint64_t bitmap_bytes = f->words * 4 * (f->pristine ? 1 : 2);
     return npos >= (uint64_t(1) << 16) && npos * 64 >= bitmap_bytes;
+}
+
+bool want_tiled_probe(pbf_filter_t* f, uint64_t n) {
+    if (!f->tiled_ok || f->k == 0 || f->k > 32 || f->tm.tb > kSlotShift) return false;
+    if (f->probe_mode == PBF_PROBE_TILED) return true;
+    if (f->probe_mode == PBF_PROBE_DIRECT) return false;
+    // direct: ~(1..k) random 64-B fabric requests per key; tiled: ~12 streamed bytes per
+    // position + one pass over the bitmap.
+    const uint64_t npos = n * f->k;
+    return npos >= (uint64_t(1) << 20) && npos * 16 >= f->words * 4;
 }
 
 int add_device(pbf_filter_t* f, const Batch& b) {
@@ -331,12 +413,28 @@ int probe_device(pbf_filter_t* f, const Batch& b, uint8_t* hitmask_dev) {
     if (b.n == 0) return PBF_OK;
     int rc = materialise(f);
     if (rc) return rc;
+    if (want_tiled_probe(f, b.n)) {
+        const uint64_t per = std::max<uint64_t>(64, (kMaxPositions / f->k) & ~uint64_t(63));
+        for (uint64_t i0 = 0; i0 < b.n; i0 += per) {
+            Batch c = b;
+            c.n = std::min<uint64_t>(per, b.n - i0);
+            if (b.km == kVar)
+                c.ks.offsets = b.ks.offsets + i0;
+            else
+                c.ks.data = b.ks.data + i0 * b.ks.key_len;
+            rc = run_tiled_probe(f, c, hitmask_dev + i0 / 8);
+            if (rc) return rc;
+        }
+        f->last_probe_mode = PBF_PROBE_TILED;
+        return PBF_OK;
+    }
     const uint32_t grid = grid_for(b.n, 256, 1u << 20);
     dispatch(kmax_for(f->k), b.km, [&](auto KMAX, auto KM) {
         k_probe<decltype(KMAX)::value, decltype(KM)::value>
-            <<<grid, 256, 0, f->stream>>>(b.ks, b.n, int(f->k), f->im, f->bitmap, hitmask_dev);
+            <<<grid, 256, 0, f->stream>>>(b.ks, b.n, int(f->k), f->im, f->bitmap, hitmask_dev, probe_stage1());
     });
     CHECK_LAUNCH();
+    f->last_probe_mode = PBF_PROBE_DIRECT;
     return PBF_OK;
 }
 
@@ -526,7 +624,7 @@ int pbf_create(int device, uint64_t nb_bytes, uint32_t nb_hash_functions, pbf_fi
         if (delta % 32) f->tiled_ok = false;
         tm.delta_words = delta / 32;
     }
-    if (tm.nbuckets > 8192) f->tiled_ok = false;  // LDS budget of k_scatter
+    if (tm.nbuckets > 8192) f->tiled_ok = false;  // LDS budget of k_part
     f->tm = tm;
     hipError_t e = hipStreamCreateWithFlags(&f->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipMalloc(&f->bitmap, f->alloc_words * 4);
@@ -560,10 +658,7 @@ int pbf_destroy(pbf_filter_t* f) {
     if (f->stream) (void)hipStreamSynchronize(f->stream);
     if (f->bitmap) (void)hipFree(f->bitmap);
     if (f->dpop) (void)hipFree(f->dpop);
-    f->positions.release();
-    f->counts.release();
-    f->total.release();
-    f->base.release();
+    for (DevBuf* d : {&f->regions, &f->fill, &f->ovf, &f->ovf_count, &f->subcnt, &f->rbits, &f->neg}) d->release();
     f->dkeys.release();
     f->doffs.release();
     f->dout.release();
@@ -701,12 +796,24 @@ void* pbf_device_bitmap(pbf_filter_t* f) {
 int pbf_set_build_mode(pbf_filter_t* f, int mode) {
     if (!f) return fail(PBF_ERR_INVALID, "null filter handle");
     if (mode < PBF_BUILD_AUTO || mode > PBF_BUILD_TILED) return fail(PBF_ERR_INVALID, "bad build mode");
-    if (mode == PBF_BUILD_TILED && !f->tiled_ok) return fail(PBF_ERR_INVALID, "tiled build unsupported for this m");
+    if (mode == PBF_BUILD_TILED && (!f->tiled_ok || f->k > 32))
+        return fail(PBF_ERR_INVALID, "tiled build unsupported for this m / k");
     f->mode = mode;
     return PBF_OK;
 }
 
 int pbf_last_build_mode(pbf_filter_t* f) { return f ? f->last_mode : 0; }
+
+int pbf_set_probe_mode(pbf_filter_t* f, int mode) {
+    if (!f) return fail(PBF_ERR_INVALID, "null filter handle");
+    if (mode < PBF_PROBE_AUTO || mode > PBF_PROBE_TILED) return fail(PBF_ERR_INVALID, "bad probe mode");
+    if (mode == PBF_PROBE_TILED && (!f->tiled_ok || f->k > 32 || f->tm.tb > kSlotShift))
+        return fail(PBF_ERR_INVALID, "tiled probe unsupported for this m / k");
+    f->probe_mode = mode;
+    return PBF_OK;
+}
+
+int pbf_last_probe_mode(pbf_filter_t* f) { return f ? f->last_probe_mode : 0; }
 
 int pbf_gen_splitmix_hex(int device, void* stream, uint8_t* out_dev, uint64_t seed, uint64_t start, uint64_t n) {
     HIP_TRY(hipSetDevice(device));

@@ -1,0 +1,493 @@
+// LDS-tiled bloom build and probe for gfx950 (reference semantics: src/bloom_filter.py:60-74).
+//
+// Random 4-byte read-modify-writes / reads into a 128 MiB bitmap are bound by the fabric's
+// request rate (measured ~55 G 64-B requests/s chip-wide), not by HBM bytes.  The tiled path
+// turns them into streams:
+//
+//   positions   A key's k hash positions.  For m <= 2^32 a position is the bit index (u32).
+//               For m > 2^32 only [0, 2^31) U [m - 2^31, m) is reachable (|h| <= 2^31): the
+//               position is u32(h) and p >= 2^31 lives at bit p + (m - 2^32).
+//   tiles       2^TB positions (TB <= 20: 128 KiB of LDS).  B = number of tiles.
+//   regions     Partition workgroup g owns one fixed-capacity region per tile: entries of
+//               (g, b) live at regions[(g*B + b)*cap ...].  No histogram pass is needed;
+//               entries beyond `cap` (only under heavy key duplication) go to an overflow list
+//               that a small fix-up kernel applies with global atomics.
+//
+// Build:  k_part<build>  hash keys in LDS-sized sub-chunks, counting-sort positions by tile
+//                        in LDS, append each tile's run to the workgroup's region.
+//         k_tile_build   one workgroup per tile: OR the tile's positions into LDS, write the
+//                        tile once (128 KiB, coalesced).
+//         k_ovf_build    global atomicOr of overflow positions (usually none).
+// Probe:  k_part<probe>  same partition; an entry is (slot-in-sub-chunk << 20 | position in
+//                        tile), and the per-sub-chunk tile counts are kept (subcnt).
+//         k_tile_probe   one workgroup per tile: load the bitmap tile into LDS, test every
+//                        entry, write one result bit per entry (R, parallel to regions).
+//         k_gather       workgroup g replays its sub-chunks: AND the result bits per key
+//                        in LDS, wave64 ballot → hit-mask words.
+//         Overflowed probe entries are tested directly against the bitmap inside k_part; a
+//         miss sets the key's bit in `neg`, which k_gather folds in.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "bloom_kernels.hpp"
+
+namespace pbf {
+
+struct TileMap {
+    IndexMap im;
+    uint32_t tb;           // log2 positions per tile (<= 20)
+    uint32_t nbuckets;     // B
+    uint32_t cspace;       // 1 when m > 2^32
+    uint32_t pad;
+    uint64_t delta_words;  // (m - 2^32) / 32 when cspace
+    uint64_t total_words;  // ceil(nb_bytes / 4)
+};
+
+struct PartGeom {
+    uint32_t G;     // partition workgroups
+    uint32_t cap;   // region capacity in entries (multiple of 32)
+    uint32_t kps;   // keys per sub-chunk (multiple of 64, <= 2048 for probes)
+    uint32_t nsub;  // sub-chunks per workgroup
+    uint64_t kpw;   // keys per workgroup (= nsub * kps)
+};
+
+constexpr uint32_t kSlotShift = 20;   // probe entry = slot-in-sub-chunk << 20 | position in tile
+constexpr uint32_t kSlotMask = 0xFFFu;  // <= 4096 keys per probe sub-chunk
+
+__device__ __forceinline__ uint32_t tile_pos(uint32_t h, const TileMap& tm) {
+    return tm.cspace ? h : uint32_t(py_index(h, tm.im));
+}
+
+__device__ __forceinline__ uint64_t pos_to_bit(uint32_t p, const TileMap& tm) {
+    uint64_t b = p;
+    if (tm.cspace && p >= 0x80000000u) b += tm.delta_words * 32;
+    return b;
+}
+
+__device__ __forceinline__ uint64_t tile_word0(uint32_t t, const TileMap& tm) {
+    const uint64_t p0 = uint64_t(t) << tm.tb;
+    uint64_t w = p0 >> 5;
+    if (tm.cspace && p0 >= (1ull << 31)) w += tm.delta_words;
+    return w;
+}
+
+// Barrier for LDS hand-offs only: waits for this wave's LDS/scalar operations, not for its
+// global stores (which __syncthreads' workgroup-release fence would drain every time).
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// Block-wide exclusive scan of a[0..B) (LDS) into out[0..B] (LDS), out[B] = total.
+// blockDim a multiple of 64, <= 1024; warp_sums holds blockDim/64 entries.  Ends synced.
+__device__ __forceinline__ void block_exclusive_scan(const uint32_t* a, uint32_t* out, uint32_t B,
+                                                     uint32_t* warp_sums) {
+    const uint32_t nt = blockDim.x, tid = threadIdx.x;
+    const uint32_t per = (B + nt - 1) / nt;
+    const uint32_t lo = min(B, tid * per), hi = min(B, lo + per);
+    uint32_t sum = 0;
+    for (uint32_t j = lo; j < hi; ++j) sum += a[j];
+    uint32_t v = sum;
+    const uint32_t lane = tid & 63;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = __shfl_up(v, d, 64);
+        if (lane >= uint32_t(d)) v += o;
+    }
+    if (lane == 63) warp_sums[tid >> 6] = v;
+    lds_barrier();
+    if (tid < 64) {
+        const uint32_t nw = nt >> 6;
+        uint32_t w = tid < nw ? warp_sums[tid] : 0u;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t o = __shfl_up(w, d, 64);
+            if (tid >= uint32_t(d)) w += o;
+        }
+        if (tid < nw) warp_sums[tid] = w;
+    }
+    lds_barrier();
+    uint32_t run = v - sum + ((tid >> 6) ? warp_sums[(tid >> 6) - 1] : 0u);
+    for (uint32_t j = lo; j < hi; ++j) {
+        const uint32_t x = a[j];
+        out[j] = run;
+        run += x;
+    }
+    if (tid == nt - 1) out[B] = run;
+    lds_barrier();
+}
+
+// Largest b in [0, B) with a[b] <= e (a non-decreasing, a[0] = 0 <= e).
+__device__ __forceinline__ uint32_t bucket_of(const uint32_t* a, uint32_t B, uint32_t e) {
+    uint32_t lo = 0, len = B;
+    while (len > 1) {
+        const uint32_t half = len >> 1;
+        if (a[lo + half] <= e) lo += half;
+        len -= half;
+    }
+    return lo;
+}
+
+// ------------------------------------------------------------------ partition
+// One 1024-thread workgroup per CU.  Each thread keeps up to KPT keys' KMAX (position, rank)
+// pairs in registers between the counting pass and the LDS placement, so every key is hashed
+// once; pg.kps = kpt_eff * 1024 keys per sub-chunk (kpt_eff <= KPT chosen by the host so the
+// stage fits LDS).  Each tile's run of a sub-chunk is written by one wave as one contiguous
+// store (runs of ~E/B entries), which keeps HBM write requests whole.
+constexpr int kPartThreads = 1024;
+__host__ __device__ constexpr int part_kpt(int kmax, int km, bool probe) {
+    // sized so every (KMAX, key mode) variant stays within 128 VGPRs without spilling
+    if (km == kFixed16) {
+        if (kmax <= 4) return probe ? 4 : 6;
+        if (kmax <= 8) return probe ? 3 : 4;
+        return kmax <= 16 ? 2 : 1;
+    }
+    return kmax <= 4 ? 4 : (kmax <= 8 ? 2 : 1);
+}
+
+template <int KMAX, int KM, bool PROBE>
+__global__ void __launch_bounds__(kPartThreads) k_part(KeySet ks, uint64_t n, int k, TileMap tm, PartGeom pg,
+                                                       uint32_t* __restrict__ regions, uint32_t* __restrict__ fill,
+                                                       uint32_t* __restrict__ subcnt, uint32_t* __restrict__ ovf,
+                                                       uint32_t* __restrict__ ovf_count,
+                                                       const uint32_t* __restrict__ bitmap, uint32_t* __restrict__ neg) {
+    constexpr int KPT = part_kpt(KMAX, KM, PROBE);
+    extern __shared__ uint32_t smem[];
+    const uint32_t B = tm.nbuckets;
+    const uint32_t tid = threadIdx.x, nt = blockDim.x;
+    const uint32_t lane = tid & 63, wave = tid >> 6, nwaves = nt >> 6;
+    const uint32_t kpt = pg.kps / nt;  // <= KPT
+    const uint32_t g = blockIdx.x;
+    uint32_t* cursor = smem;           // B: entries routed to (g, b) so far
+    uint32_t* cnt = cursor + B;        // B: this sub-chunk's per-tile count
+    uint32_t* lbase = cnt + B;         // B+1
+    uint32_t* ws = lbase + B + 1;      // 16
+    uint32_t* stage = ws + 16;         // kps * k
+    const uint32_t lmask = (1u << tm.tb) - 1u;
+    for (uint32_t b = tid; b < B; b += nt) cursor[b] = 0;
+    const uint64_t k0 = uint64_t(g) * pg.kpw;
+    const uint64_t k1 = min(n, k0 + pg.kpw);
+    // fixed 16-byte keys: the next sub-chunk's keys are loaded during this one's write-out
+    uint4 kw[KM == kFixed16 ? KPT : 1];
+    auto load_keys = [&](uint64_t s0) {
+        if constexpr (KM == kFixed16) {
+#pragma unroll
+            for (int u = 0; u < KPT; ++u) {
+                const uint64_t i = min(s0 + u * nt + tid, n - 1);
+                kw[u] = reinterpret_cast<const uint4*>(ks.data)[i];
+            }
+        }
+    };
+    if (k0 < k1) load_keys(k0);
+    uint32_t j = 0;
+    for (uint64_t s0 = k0; s0 < k1; s0 += pg.kps, ++j) {
+        const uint64_t s1 = min(k1, s0 + pg.kps);
+        for (uint32_t b = tid; b < B; b += nt) cnt[b] = 0;
+        lds_barrier();
+        uint32_t pos[KPT * KMAX], rk[KPT * KMAX];
+#pragma unroll
+        for (int u = 0; u < KPT; ++u) {
+            const uint64_t i = s0 + u * nt + tid;
+            auto emit = [&](int s, uint32_t h) {
+                const uint32_t p = tile_pos(h, tm);
+                pos[u * KMAX + s] = p;
+                rk[u * KMAX + s] = atomicAdd(cnt + (p >> tm.tb), 1u);
+            };
+            if (uint32_t(u) < kpt && i < s1) {
+                if constexpr (KM == kFixed16)
+                    murmur_seeds16<KMAX>(kw[u], k, emit);
+                else
+                    hash_key<KMAX, KM>(ks, i, k, emit);
+            }
+        }
+        lds_barrier();
+        if constexpr (PROBE) {
+            uint32_t* sc = subcnt + (uint64_t(g) * pg.nsub + j) * B;
+            for (uint32_t b = tid; b < B; b += nt) sc[b] = cnt[b];
+        }
+        block_exclusive_scan(cnt, lbase, B, ws);
+#pragma unroll
+        for (int u = 0; u < KPT; ++u) {
+            const uint32_t slot_key = u * nt + tid;
+            if (uint32_t(u) < kpt && s0 + slot_key < s1) {
+#pragma unroll
+                for (int s = 0; s < KMAX; ++s) {
+                    if (s < k) {
+                        const uint32_t p = pos[u * KMAX + s];
+                        const uint32_t slot = lbase[p >> tm.tb] + rk[u * KMAX + s];
+                        stage[slot] = PROBE ? ((slot_key << kSlotShift) | (p & lmask)) : p;
+                    }
+                }
+            }
+        }
+        lds_barrier();
+        if (s0 + pg.kps < k1) load_keys(s0 + pg.kps);
+        // one wave per tile run: contiguous stores into region (g, b)
+        for (uint32_t b = wave; b < B; b += nwaves) {
+            const uint32_t lb = lbase[b], len = lbase[b + 1] - lb, cur = cursor[b];
+            uint32_t* dst = regions + (uint64_t(g) * B + b) * pg.cap;
+            for (uint32_t i = lane; i < len; i += 64) {
+                const uint32_t v = stage[lb + i];
+                const uint32_t r = cur + i;
+                if (r < pg.cap) {
+                    dst[r] = v;
+                } else if constexpr (PROBE) {
+                    const uint64_t bit = pos_to_bit((b << tm.tb) | (v & lmask), tm);
+                    if (!((bitmap[bit >> 5] >> (bit & 31)) & 1u)) {
+                        const uint64_t key = s0 + (v >> kSlotShift);
+                        atomicOr(neg + (key >> 5), 1u << (key & 31));
+                    }
+                } else {
+                    ovf[atomicAdd(ovf_count, 1u)] = v;
+                }
+            }
+            if (lane == 0) cursor[b] = cur + len;
+        }
+    }
+    lds_barrier();
+    for (uint32_t b = tid; b < B; b += nt) fill[uint64_t(b) * pg.G + g] = min(cursor[b], pg.cap);
+}
+
+// Copy nw words of the bitmap starting at word w0 into LDS (zero-filling up to W), with every
+// thread's loads issued before any is consumed.
+__device__ __forceinline__ void load_tile(uint32_t* tile, const uint32_t* __restrict__ bitmap, uint64_t w0,
+                                          uint32_t nw, uint32_t W) {
+    const uint32_t tid = threadIdx.x, nt = blockDim.x;
+    if ((w0 & 3) == 0 && nw == W) {
+        // loads are unconditional (clamped index) so the batch stays in registers
+        const uint4* src = reinterpret_cast<const uint4*>(bitmap + w0);
+        const uint32_t W4 = W / 4;
+        for (uint32_t q0 = tid; q0 < W4; q0 += nt * 8) {
+            uint4 v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = src[min(q0 + u * nt, W4 - 1)];
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (q0 + u * nt < W4) reinterpret_cast<uint4*>(tile)[q0 + u * nt] = v[u];
+        }
+    } else {
+        for (uint32_t w = tid; w < W; w += nt) tile[w] = w < nw ? bitmap[w0 + w] : 0u;
+    }
+}
+
+__device__ __forceinline__ void store_tile(const uint32_t* tile, uint32_t* __restrict__ bitmap, uint64_t w0,
+                                           uint32_t nw) {
+    const uint32_t tid = threadIdx.x, nt = blockDim.x;
+    if ((w0 & 3) == 0 && (nw & 3) == 0) {
+        uint4* dst = reinterpret_cast<uint4*>(bitmap + w0);
+        for (uint32_t q = tid; q < nw / 4; q += nt) dst[q] = reinterpret_cast<const uint4*>(tile)[q];
+    } else {
+        for (uint32_t w = tid; w < nw; w += nt) bitmap[w0 + w] = tile[w];
+    }
+}
+
+__device__ __forceinline__ void or_bits4(uint32_t* tile, uint4 v, uint32_t e, uint32_t f, uint32_t lmask) {
+    uint32_t p = v.x & lmask;
+    if (e < f) atomicOr(tile + (p >> 5), 1u << (p & 31));
+    p = v.y & lmask;
+    if (e + 1 < f) atomicOr(tile + (p >> 5), 1u << (p & 31));
+    p = v.z & lmask;
+    if (e + 2 < f) atomicOr(tile + (p >> 5), 1u << (p & 31));
+    p = v.w & lmask;
+    if (e + 3 < f) atomicOr(tile + (p >> 5), 1u << (p & 31));
+}
+
+// ------------------------------------------------------------------ build: tiles
+// One workgroup per tile.  A wave (64 lanes x 16-byte loads = 256 entries) covers one region
+// per step and keeps U regions of loads in flight.
+__global__ void __launch_bounds__(1024) k_tile_build(TileMap tm, PartGeom pg, const uint32_t* __restrict__ regions,
+                                                     const uint32_t* __restrict__ fill, uint32_t* __restrict__ bitmap,
+                                                     int pristine) {
+    extern __shared__ uint32_t smem[];
+    const uint32_t B = tm.nbuckets, G = pg.G, cap = pg.cap;
+    const uint32_t b = blockIdx.x;
+    const uint32_t W = 1u << (tm.tb - 5);
+    uint32_t* tile = smem;       // W
+    uint32_t* fills = tile + W;  // G
+    const uint64_t w0 = tile_word0(b, tm);
+    const uint32_t nw = uint32_t(min<uint64_t>(W, tm.total_words - w0));
+    const uint32_t tid = threadIdx.x, nt = blockDim.x;
+    for (uint32_t q = tid; q < G; q += nt) fills[q] = fill[uint64_t(b) * G + q];
+    if (pristine) {
+        for (uint32_t q = tid; q < W / 4; q += nt) reinterpret_cast<uint4*>(tile)[q] = make_uint4(0, 0, 0, 0);
+    } else {
+        load_tile(tile, bitmap, w0, nw, W);
+    }
+    lds_barrier();
+    const uint32_t lane = tid & 63, wave = tid >> 6, nwaves = nt >> 6;
+    const uint32_t lmask = (1u << tm.tb) - 1u;
+    const uint32_t lc = min(lane, cap / 4 - 1);  // unconditional loads stay inside the region
+    constexpr int U = 4;
+    for (uint32_t g0 = wave; g0 < G; g0 += nwaves * U) {
+        uint4 v[U];
+        uint32_t f[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t q = g0 + u * nwaves;
+            f[u] = q < G ? fills[q] : 0u;
+            v[u] = reinterpret_cast<const uint4*>(regions + (uint64_t(min(q, G - 1)) * B + b) * cap)[lc];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (lane * 4 < f[u]) or_bits4(tile, v[u], lane * 4, f[u], lmask);
+    }
+    // regions holding more than 256 entries
+    if (cap > 256) {
+        for (uint32_t q = wave; q < G; q += nwaves) {
+            const uint32_t fq = fills[q];
+            for (uint32_t c = 64 + lane; c * 4 < fq; c += 64)
+                or_bits4(tile, reinterpret_cast<const uint4*>(regions + (uint64_t(q) * B + b) * cap)[c], c * 4, fq,
+                         lmask);
+        }
+    }
+    lds_barrier();
+    store_tile(tile, bitmap, w0, nw);
+}
+
+__global__ void __launch_bounds__(256) k_ovf_build(TileMap tm, const uint32_t* __restrict__ ovf,
+                                                   const uint32_t* __restrict__ ovf_count, uint32_t* __restrict__ bitmap) {
+    const uint32_t cnt = *ovf_count;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < cnt; i += gridDim.x * blockDim.x) {
+        const uint64_t bit = pos_to_bit(ovf[i], tm);
+        atomicOr(bitmap + (bit >> 5), 1u << (bit & 31));
+    }
+}
+
+// ------------------------------------------------------------------ probe: tiles
+// One workgroup per tile.  A work item is one 32-entry word of one region: 8 16-byte loads,
+// 32 LDS bit tests, one 4-byte store of result bits into R[(g*B + b)*(cap/32) + word].  Each
+// thread issues two work items' loads before testing either.  `expand` = the LDS budget allows
+// a per-word region id table (else a binary search over the word prefix).
+__global__ void __launch_bounds__(1024) k_tile_probe(TileMap tm, PartGeom pg, const uint32_t* __restrict__ regions,
+                                                     const uint32_t* __restrict__ fill,
+                                                     const uint32_t* __restrict__ bitmap, uint32_t* __restrict__ R,
+                                                     int expand) {
+    extern __shared__ uint32_t smem[];
+    const uint32_t B = tm.nbuckets, G = pg.G, cap = pg.cap, wpr = cap / 32;
+    const uint32_t b = blockIdx.x;
+    const uint32_t W = 1u << (tm.tb - 5);
+    uint32_t* tile = smem;          // W
+    uint32_t* fills = tile + W;     // G
+    uint32_t* wpre = fills + G;     // G+1
+    uint32_t* ws = wpre + G + 1;    // 16
+    uint16_t* wq = reinterpret_cast<uint16_t*>(ws + 16);  // G*wpr (expand)
+    const uint64_t w0 = tile_word0(b, tm);
+    const uint32_t nw = uint32_t(min<uint64_t>(W, tm.total_words - w0));
+    const uint32_t tid = threadIdx.x, nt = blockDim.x;
+    for (uint32_t q = tid; q < G; q += nt) fills[q] = (fill[uint64_t(b) * G + q] + 31) >> 5;  // words
+    load_tile(tile, bitmap, w0, nw, W);
+    lds_barrier();
+    block_exclusive_scan(fills, wpre, G, ws);
+    for (uint32_t q = tid; q < G; q += nt) {
+        fills[q] = fill[uint64_t(b) * G + q];  // entries again
+        if (expand)
+            for (uint32_t c = wpre[q]; c < wpre[q + 1]; ++c) wq[c] = uint16_t(q);
+    }
+    lds_barrier();
+    const uint32_t lmask = (1u << tm.tb) - 1u;
+    const uint32_t total = wpre[G];
+    constexpr int U = 2;
+    for (uint32_t c0 = tid; c0 < total; c0 += nt * U) {
+        uint4 v[U][8];
+        uint32_t qq[U], word[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t c = min(c0 + u * nt, total - 1);  // unconditional loads stay in registers
+            qq[u] = expand ? uint32_t(wq[c]) : bucket_of(wpre, G, c);
+            word[u] = c - wpre[qq[u]];
+            const uint4* src = reinterpret_cast<const uint4*>(regions + (uint64_t(qq[u]) * B + b) * cap + word[u] * 32);
+#pragma unroll
+            for (int t = 0; t < 8; ++t) v[u][t] = src[t];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t c = c0 + u * nt;
+            if (c < total) {
+                const uint32_t f = fills[qq[u]];
+                const uint32_t e0 = word[u] * 32;
+                uint32_t bits = 0;
+#pragma unroll
+                for (int t = 0; t < 8; ++t) {
+                    uint32_t p = v[u][t].x & lmask;
+                    bits |= ((tile[p >> 5] >> (p & 31)) & 1u) << (t * 4);
+                    p = v[u][t].y & lmask;
+                    bits |= ((tile[p >> 5] >> (p & 31)) & 1u) << (t * 4 + 1);
+                    p = v[u][t].z & lmask;
+                    bits |= ((tile[p >> 5] >> (p & 31)) & 1u) << (t * 4 + 2);
+                    p = v[u][t].w & lmask;
+                    bits |= ((tile[p >> 5] >> (p & 31)) & 1u) << (t * 4 + 3);
+                }
+                if (f - e0 < 32) bits &= (1u << (f - e0)) - 1u;  // entries past the fill
+                R[(uint64_t(qq[u]) * B + b) * wpr + word[u]] = bits;
+            }
+        }
+    }
+}
+
+// Workgroup g replays its sub-chunks (same geometry as k_part<probe>).  One wave per tile reads
+// the sub-chunk's in-region run of (g, b) and its result bits, and clears the flag of every key
+// with a 0 bit; then the sub-chunk's keys are balloted into hit-mask words.
+__global__ void __launch_bounds__(1024) k_gather(TileMap tm, PartGeom pg, uint64_t n,
+                                                 const uint32_t* __restrict__ regions, const uint32_t* __restrict__ R,
+                                                 const uint32_t* __restrict__ subcnt, const uint32_t* __restrict__ neg,
+                                                 uint8_t* __restrict__ hitmask) {
+    extern __shared__ uint32_t smem[];
+    const uint32_t B = tm.nbuckets, cap = pg.cap, wpr = cap / 32;
+    const uint32_t tid = threadIdx.x, nt = blockDim.x;
+    const uint32_t lane = tid & 63, wave = tid >> 6, nwaves = nt >> 6;
+    const uint32_t g = blockIdx.x;
+    uint32_t* cursor = smem;         // B
+    uint32_t* cnt = cursor + B;      // B
+    uint32_t* flags = cnt + B;       // kps
+    for (uint32_t b = tid; b < B; b += nt) cursor[b] = 0;
+    const uint64_t k0 = uint64_t(g) * pg.kpw;
+    const uint64_t k1 = min(n, k0 + pg.kpw);
+    uint32_t j = 0;
+    for (uint64_t s0 = k0; s0 < k1; s0 += pg.kps, ++j) {
+        const uint32_t nk = uint32_t(min<uint64_t>(k1 - s0, pg.kps));
+        const uint32_t* sc = subcnt + (uint64_t(g) * pg.nsub + j) * B;
+        lds_barrier();
+        for (uint32_t b = tid; b < B; b += nt) cnt[b] = sc[b];
+        for (uint32_t s = tid; s < pg.kps; s += nt) {
+            const uint64_t key = s0 + s;
+            flags[s] = (s < nk && !((neg[key >> 5] >> (key & 31)) & 1u)) ? 1u : 0u;
+        }
+        lds_barrier();
+        constexpr int U = 4;
+        for (uint32_t b0 = wave; b0 < B; b0 += nwaves * U) {
+            uint32_t v[U], rw[U], len[U], r[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t b = min(b0 + u * nwaves, B - 1);
+                const uint32_t cur = cursor[b];
+                len[u] = (b0 + u * nwaves < B && cur < cap) ? min(cnt[b], cap - cur) : 0u;
+                r[u] = min(cur + lane, cap - 1);  // unconditional loads stay inside the region
+                const uint64_t reg = uint64_t(g) * B + b;
+                v[u] = regions[reg * cap + r[u]];
+                rw[u] = R[reg * wpr + (r[u] >> 5)];
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (lane < len[u] && !((rw[u] >> (r[u] & 31)) & 1u)) flags[(v[u] >> kSlotShift) & kSlotMask] = 0u;
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t b = b0 + u * nwaves;
+                if (b < B) {
+                    const uint32_t cur = cursor[b];
+                    const uint64_t reg = uint64_t(g) * B + b;
+                    for (uint32_t i = 64 + lane; i < len[u]; i += 64) {  // runs longer than a wave
+                        const uint32_t rr = cur + i;
+                        if (!((R[reg * wpr + (rr >> 5)] >> (rr & 31)) & 1u))
+                            flags[(regions[reg * cap + rr] >> kSlotShift) & kSlotMask] = 0u;
+                    }
+                    if (lane == 0) cursor[b] = cur + cnt[b];
+                }
+            }
+        }
+        lds_barrier();
+        for (uint32_t s = tid; s < ((nk + 63) & ~63u); s += nt) {
+            const unsigned long long bal = __ballot(s < nk && flags[s] != 0u);
+            if ((s & 63) == 0) store_hit_word(hitmask, n, s0 + s, bal);
+        }
+    }
+}
+
+}  // namespace pbf

@@ -5,7 +5,7 @@ import pytest
 
 from pebbledb_amd import BloomFilter, PackedKeys
 from pebbledb_amd import _native
-from pebbledb_amd._native import PBF_BUILD_ATOMIC, PBF_BUILD_TILED
+from pebbledb_amd._native import PBF_BUILD_ATOMIC, PBF_BUILD_TILED, PBF_PROBE_DIRECT, PBF_PROBE_TILED
 from pebbledb_amd.keys import splitmix_hex_keys, varlen_keys
 
 pytestmark = pytest.mark.gpu
@@ -42,12 +42,17 @@ def test_device_resident_equals_host_path(oracle, mode):
     q = dev_keys_hex(9, n // 2, n)
     hm = torch.zeros((n + 7) // 8, dtype=torch.uint8, device="cuda")
     torch.cuda.synchronize()
-    bf.probe_device_fixed(q.data_ptr(), 16, n, hm.data_ptr())
-    bf.sync()
     want = oracle.build(2 ** 18, 6, host)
-    assert bf.bitmap() == want.tobytes()
     qh = PackedKeys.fixed(splitmix_hex_keys(9, n // 2, n))
-    assert np.array_equal(hm.cpu().numpy(), oracle.probe(want, 6, qh))
+    want_hm = oracle.probe(want, 6, qh)
+    for pm in (PBF_PROBE_DIRECT, PBF_PROBE_TILED):
+        hm.zero_()
+        torch.cuda.synchronize()
+        bf.set_probe_mode(pm)
+        bf.probe_device_fixed(q.data_ptr(), 16, n, hm.data_ptr())
+        bf.sync()
+        assert bf.bitmap() == want.tobytes()
+        assert np.array_equal(hm.cpu().numpy(), want_hm), pm
     # variable-length on device, offsets not starting at 0 (a slice of a larger batch)
     d, o = varlen_keys(21, 0, 30001)
     od = torch.from_numpy(o.view(np.int64)).cuda()
@@ -84,9 +89,17 @@ def test_config2_full_size_properties(oracle):
     q = dev_keys_hex(0x5EEDB100, 0, 2 * n)
     hm = torch.zeros(2 * n // 8, dtype=torch.uint8, device="cuda")
     torch.cuda.synchronize()
+    a.set_probe_mode(PBF_PROBE_TILED)
     a.probe_device_fixed(q.data_ptr(), 16, 2 * n, hm.data_ptr())
     a.sync()
+    assert a.last_probe_mode == PBF_PROBE_TILED
     h = hm.cpu().numpy()
+    hm2 = torch.zeros(2 * n // 8, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    a.set_probe_mode(PBF_PROBE_DIRECT)
+    a.probe_device_fixed(q.data_ptr(), 16, 2 * n, hm2.data_ptr())
+    a.sync()
+    assert np.array_equal(hm2.cpu().numpy(), h)  # direct == tiled at full size
     assert (h[: n // 8] == 0xFF).all()  # no false negatives
     fp = int(np.unpackbits(h[n // 8:]).sum())
     fill = a.popcount() / (8 * nb)

@@ -7,18 +7,44 @@ import pytest
 
 from conftest import load_golden
 from pebbledb_amd import BloomFilter, PackedKeys
-from pebbledb_amd._native import PBF_BUILD_ATOMIC, PBF_BUILD_AUTO, PBF_BUILD_TILED
+from pebbledb_amd._native import (PBF_BUILD_ATOMIC, PBF_BUILD_AUTO, PBF_BUILD_TILED, PBF_PROBE_DIRECT,
+                                  PBF_PROBE_TILED)
 from pebbledb_amd.keys import splitmix_hex_keys, varlen_keys
 
 pytestmark = pytest.mark.gpu
 
 MODES = [PBF_BUILD_ATOMIC, PBF_BUILD_TILED]
+PROBE_MODES = [PBF_PROBE_DIRECT, PBF_PROBE_TILED]
+
+
+def probe_both(bf, keys):
+    """Hit mask from the direct AND the tiled probe; they must agree bit for bit."""
+    pk = keys if isinstance(keys, PackedKeys) else PackedKeys.from_strs(list(keys))
+    out = []
+    for pm in PROBE_MODES:
+        try:
+            bf.set_probe_mode(pm)
+        except ValueError:  # the tiled probe needs k <= 32 (register budget of k_part)
+            assert pm == PBF_PROBE_TILED and bf.nb_hash_functions > 32
+            continue
+        out.append(bf.may_contain_many(pk, packed=True))
+        if pk.n:
+            assert bf.last_probe_mode == pm
+    bf.set_probe_mode(0)
+    assert all(np.array_equal(out[0], o) for o in out[1:]), "direct and tiled probes disagree"
+    return out[0]
 
 
 def built(nb, k, keys, mode=PBF_BUILD_AUTO):
     bf = BloomFilter(nb, k)
     if mode != PBF_BUILD_AUTO:
-        bf.set_build_mode(mode)
+        try:
+            bf.set_build_mode(mode)
+        except ValueError:  # the tiled build needs k <= 32
+            assert mode == PBF_BUILD_TILED and k > 32
+    bf.add_many(keys)
+    if mode != PBF_BUILD_AUTO and len(keys if not isinstance(keys, PackedKeys) else range(keys.n)) and k <= 32:
+        assert bf.last_build_mode == mode
     bf.add_many(keys)
     return bf
 
@@ -129,7 +155,7 @@ def test_config1_golden(mode):
     keys = [f"{i:016d}" for i in range(1000)]
     bf = built(1024, 4, keys, mode)
     _check_desc(bf, g["config1"])
-    hm = bf.may_contain_many([f"{i:016d}" for i in range(11000)], packed=True)
+    hm = probe_both(bf, [f"{i:016d}" for i in range(11000)])
     assert hm.tobytes().hex() == g["config1"]["probe_hitmask_hex"]
     bfp = BloomFilter.build_from_keys_and_fp_rate(keys, 0.001)
     _check_desc(bfp, g["product_p0001"])
@@ -142,10 +168,10 @@ def test_splitmix_golden(mode):
     non = PackedKeys.fixed(splitmix_hex_keys(g["seed"], g["nonmember_start"], g["nonmembers"]))
     bf = built(8192, 6, members, mode)
     _check_desc(bf, g["pow2"])
-    assert bf.may_contain_many(non, packed=True).tobytes().hex() == g["pow2"]["hitmask_nonmembers_hex"]
+    assert probe_both(bf, non).tobytes().hex() == g["pow2"]["hitmask_nonmembers_hex"]
     bf2 = built(6007, 7, PackedKeys.fixed(splitmix_hex_keys(g["seed"], 0, 5000)), mode)
     _check_desc(bf2, g["odd"])
-    assert bf2.may_contain_many(non, packed=True).tobytes().hex() == g["odd"]["hitmask_nonmembers_hex"]
+    assert probe_both(bf2, non).tobytes().hex() == g["odd"]["hitmask_nonmembers_hex"]
 
 
 @pytest.mark.parametrize("mode", MODES)
@@ -155,14 +181,14 @@ def test_varlen_and_unicode_golden(mode):
     bf = built(8192, 8, PackedKeys(d, g["members"], offsets=o), mode)
     _check_desc(bf, g["varlen"])
     d2, o2 = varlen_keys(g["seed"], g["nonmember_start"], g["nonmembers"])
-    hm = bf.may_contain_many(PackedKeys(d2, g["nonmembers"], offsets=o2), packed=True)
+    hm = probe_both(bf, PackedKeys(d2, g["nonmembers"], offsets=o2))
     assert hm.tobytes().hex() == g["varlen"]["hitmask_nonmembers_hex"]
     sk = [(f"{i:08d}" * 8)[:8 + i % 57] for i in range(1000)]
     _check_desc(built(1024, 8, sk, mode), g["survey_family"])
     u = load_golden("unicode.json")
     bfu = built(u["nb_bytes"], u["nb_hash_functions"], u["keys"], mode)
     _check_desc(bfu, u)
-    hm = bfu.may_contain_many(u["keys"] + [f"absent-{i}" for i in range(200)], packed=True)
+    hm = probe_both(bfu, u["keys"] + [f"absent-{i}" for i in range(200)])
     assert hm.tobytes().hex() == u["hitmask_hex"]
 
 
@@ -195,7 +221,7 @@ def test_sweep_against_oracle(oracle, nb, k, kind, n):
         bf = built(nb, k, keys, mode)
         got = np.frombuffer(bf.bitmap(), dtype=np.uint8)
         assert np.array_equal(got, want), (mode, int((got != want).sum()))
-        assert np.array_equal(bf.may_contain_many(probes, packed=True), want_hm)
+        assert np.array_equal(probe_both(bf, probes), want_hm)
         del bf
 
 
@@ -269,7 +295,7 @@ def test_hitmask_tails(oracle):
     bf = built(4096, 6, keys)
     for n in (1, 7, 8, 9, 63, 64, 65, 127, 129, 1000):
         q = PackedKeys.fixed(keys.data.reshape(-1, 16)[:n])
-        assert np.array_equal(bf.may_contain_many(q, packed=True), oracle.probe(want, 6, q)), n
+        assert np.array_equal(probe_both(bf, q), oracle.probe(want, 6, q)), n
         assert bf.may_contain_many(q).all()
 
 
@@ -291,7 +317,9 @@ def test_small_host_stage_chunks(oracle, monkeypatch):
                 bf = BloomFilter(50000, 6); bf.set_build_mode(mode); bf.add_many(pk)
                 want = o.build(50000, 6, pk)
                 assert bf.bitmap() == want.tobytes()
-                assert np.array_equal(bf.may_contain_many(pk, packed=True), o.probe(want, 6, pk))
+                for pm in (1, 2):
+                    bf.set_probe_mode(pm)
+                    assert np.array_equal(bf.may_contain_many(pk, packed=True), o.probe(want, 6, pk))
         print('ok')
     """)
     env = dict(os.environ, PBF_STAGE_BYTES="4099")
