@@ -181,13 +181,14 @@ class BloomFilter:
         return self.bitmap() + encoded_nb_hash_functions
 
     @classmethod
-    def from_bytes(cls, data: bytes, device: Optional[int] = None) -> "BloomFilter":
-        """bloom_filter.py:83-90."""
+    def from_bytes(cls, data, device: Optional[int] = None) -> "BloomFilter":
+        """bloom_filter.py:83-90.  `data` may be bytes, bytearray or a memoryview slice of a
+        file buffer (uploaded without an intermediate copy)."""
         nb_bytes = len(data) - 1
-        nb_hash_functions = struct.unpack("B", data[nb_bytes:])[0]
+        nb_hash_functions = struct.unpack("B", bytes(data[nb_bytes:]))[0]
         bf = cls(nb_bytes=nb_bytes, nb_hash_functions=nb_hash_functions, device=device)
         if nb_bytes > 0:
-            arr = np.frombuffer(bytes(data[:nb_bytes]), dtype=np.uint8)
+            arr = np.frombuffer(data, dtype=np.uint8, count=nb_bytes)
             _native.check(_native.lib().pbf_set_bitmap(bf._h, _vp(arr), nb_bytes), "pbf_set_bitmap")
         return bf
 

@@ -264,12 +264,13 @@ struct PartPlan {
 PartPlan plan_partition(uint32_t B, uint32_t k, int km, uint64_t n, bool probe) {
     PartPlan pl{};
     const size_t fixed = size_t(3 * B + 1 + 16) * 4;
-    // keys per thread per sub-chunk: as many as the registers (part_kpt) and 156 KiB of LDS allow
+    const size_t per_entry = probe ? 6 : 4;  // stage u32 (+ u16 tile id for probes)
+    // keys per thread per sub-chunk: as many as the registers (part_kpt) and the LDS allow
     uint64_t kpt = uint64_t(part_kpt(kmax_for(k), km, probe));
-    while (kpt > 1 && fixed + kpt * kPartThreads * k * 4 > 156 * 1024) --kpt;
+    while (kpt > 1 && fixed + kpt * kPartThreads * k * per_entry > 156 * 1024) --kpt;
     if (probe) kpt = std::min<uint64_t>(kpt, (kSlotMask + 1) / kPartThreads);
     const uint64_t kps = kpt * kPartThreads;
-    pl.lds_part = fixed + size_t(kps) * k * 4;
+    pl.lds_part = fixed + size_t(kps) * k * per_entry;
     const uint64_t G0 = std::min<uint64_t>(256, std::max<uint64_t>(1, (n + kps - 1) / kps));
     uint64_t kpw = (n + G0 - 1) / G0;
     kpw = ((kpw + kps - 1) / kps) * kps;
@@ -359,7 +360,7 @@ int run_tiled_probe(pbf_filter_t* f, const Batch& b, uint8_t* hitmask) {
     HIP_TRY(allow_lds(k_tile_probe, lds_tile));
     k_tile_probe<<<B, 1024, lds_tile, s>>>(tm, pg, regions, fill, f->bitmap, R, expand);
     CHECK_LAUNCH();
-    const size_t lds_gather = (size_t(2) * B + pg.kps) * 4;
+    const size_t lds_gather = size_t((pg.kpw + 31) / 32) * 4 + size_t(B) * (pg.nsub + 1) * 2 + 16;
     HIP_TRY(allow_lds(k_gather, lds_gather));
     k_gather<<<pg.G, 1024, lds_gather, s>>>(tm, pg, b.n, regions, R, subcnt, neg, hitmask);
     CHECK_LAUNCH();
@@ -381,10 +382,23 @@ bool want_tiled_probe(pbf_filter_t* f, uint64_t n) {
     if (!f->tiled_ok || f->k == 0 || f->k > 32 || f->tm.tb > kSlotShift) return false;
     if (f->probe_mode == PBF_PROBE_TILED) return true;
     if (f->probe_mode == PBF_PROBE_DIRECT) return false;
-    // direct: ~(1..k) random 64-B fabric requests per key; tiled: ~12 streamed bytes per
-    // position + one pass over the bitmap.
+    // direct: ~1..k random 64-B requests per key, cheap while the bitmap stays in one XCD's
+    // 4 MiB L2; tiled: ~16 streamed bytes per position + one pass over the bitmap.
     const uint64_t npos = n * f->k;
-    return npos >= (uint64_t(1) << 20) && npos * 16 >= f->words * 4;
+    return f->words * 4 > (uint64_t(8) << 20) && npos >= (uint64_t(1) << 20) && npos * 16 >= f->words * 4;
+}
+
+// Largest probe batch one tiled pipeline takes: k_gather keeps a u16 run-boundary table
+// (B x (nsub+1)) and a bit per key of its workgroup in LDS, and positions stay u32.
+uint64_t tiled_probe_batch(pbf_filter_t* f, int km) {
+    const uint32_t B = f->tm.nbuckets, k = f->k;
+    uint64_t n = std::max<uint64_t>(64, (kMaxPositions / k) & ~uint64_t(63));
+    for (;;) {
+        const PartPlan pl = plan_partition(B, k, km, n, true);
+        const size_t lds = size_t((pl.pg.kpw + 31) / 32) * 4 + size_t(B) * (pl.pg.nsub + 1) * 2 + 16;
+        if ((lds <= 156 * 1024 && pl.pg.cap <= 65535) || n <= 64 * 1024) return n;
+        n = std::max<uint64_t>(64 * 1024, (n / 2) & ~uint64_t(63));
+    }
 }
 
 int add_device(pbf_filter_t* f, const Batch& b) {
@@ -414,7 +428,7 @@ int probe_device(pbf_filter_t* f, const Batch& b, uint8_t* hitmask_dev) {
     int rc = materialise(f);
     if (rc) return rc;
     if (want_tiled_probe(f, b.n)) {
-        const uint64_t per = std::max<uint64_t>(64, (kMaxPositions / f->k) & ~uint64_t(63));
+        const uint64_t per = tiled_probe_batch(f, b.km);
         for (uint64_t i0 = 0; i0 < b.n; i0 += per) {
             Batch c = b;
             c.n = std::min<uint64_t>(per, b.n - i0);
@@ -449,11 +463,22 @@ int hash_device(pbf_filter_t* f, const Batch& b, uint64_t* out_dev) {
     return PBF_OK;
 }
 
+// True when p is page-locked host memory (hipHostMalloc / hipHostRegister / torch pin_memory).
+bool is_pinned_host(const void* p) {
+    hipPointerAttribute_t a{};
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();  // pageable memory: clear the sticky error
+        return false;
+    }
+    return a.type == hipMemoryTypeHost;
+}
+
 // Host-resident keys: stream them through pinned double buffers in chunks of whole keys.
 // `op(batch_on_device, first_key_index)` runs the device work for one chunk.
 template <class Op>
 int for_host_chunks(pbf_filter_t* f, const uint8_t* keys, const uint64_t* offsets, uint32_t key_len, uint64_t n,
                     uint64_t key_align, Op&& op) {
+    const bool pinned = is_pinned_host(keys) && (!offsets || is_pinned_host(offsets));
     uint64_t i0 = 0;
     while (i0 < n) {
         // choose [i0, i1)
@@ -481,21 +506,30 @@ int for_host_chunks(pbf_filter_t* f, const uint8_t* keys, const uint64_t* offset
         const uint64_t byte0 = offsets ? offsets[i0] : i0 * key_len;
         const uint64_t nbytes = offsets ? offsets[i1] - offsets[i0] : cn * key_len;
         const size_t off_bytes = offsets ? size_t(cn + 1) * 8 : 0;
-        PinBuf& pb = f->pin[f->pin_next];
-        f->pin_next ^= 1;
-        if (pb.done) HIP_TRY(hipEventSynchronize(pb.done));
-        HIP_TRY(pb.ensure(nbytes + off_bytes + 16));
-        if (!pb.done) HIP_TRY(hipEventCreateWithFlags(&pb.done, hipEventDisableTiming));
         // device staging (single buffer: stream order serialises reuse)
         HIP_TRY(f->dkeys.ensure(((nbytes + 15) & ~uint64_t(15)) + 16));
         if (offsets) HIP_TRY(f->doffs.ensure(off_bytes));
-        std::memcpy(pb.p, keys + byte0, nbytes);
-        if (offsets) std::memcpy(static_cast<uint8_t*>(pb.p) + ((nbytes + 15) & ~uint64_t(15)), offsets + i0, off_bytes);
-        HIP_TRY(hipMemcpyAsync(f->dkeys.p, pb.p, nbytes, hipMemcpyHostToDevice, f->stream));
-        if (offsets)
-            HIP_TRY(hipMemcpyAsync(f->doffs.p, static_cast<uint8_t*>(pb.p) + ((nbytes + 15) & ~uint64_t(15)), off_bytes,
-                                   hipMemcpyHostToDevice, f->stream));
-        HIP_TRY(hipEventRecord(pb.done, f->stream));
+        if (pinned) {
+            // caller's buffers are page-locked: DMA straight from them (the call syncs before
+            // returning, so they stay valid for the copy)
+            if (nbytes) HIP_TRY(hipMemcpyAsync(f->dkeys.p, keys + byte0, nbytes, hipMemcpyHostToDevice, f->stream));
+            if (offsets)
+                HIP_TRY(hipMemcpyAsync(f->doffs.p, offsets + i0, off_bytes, hipMemcpyHostToDevice, f->stream));
+        } else {
+            PinBuf& pb = f->pin[f->pin_next];
+            f->pin_next ^= 1;
+            if (pb.done) HIP_TRY(hipEventSynchronize(pb.done));
+            HIP_TRY(pb.ensure(nbytes + off_bytes + 16));
+            if (!pb.done) HIP_TRY(hipEventCreateWithFlags(&pb.done, hipEventDisableTiming));
+            const size_t off_at = (nbytes + 15) & ~uint64_t(15);
+            std::memcpy(pb.p, keys + byte0, nbytes);
+            if (offsets) std::memcpy(static_cast<uint8_t*>(pb.p) + off_at, offsets + i0, off_bytes);
+            HIP_TRY(hipMemcpyAsync(f->dkeys.p, pb.p, nbytes, hipMemcpyHostToDevice, f->stream));
+            if (offsets)
+                HIP_TRY(hipMemcpyAsync(f->doffs.p, static_cast<uint8_t*>(pb.p) + off_at, off_bytes,
+                                       hipMemcpyHostToDevice, f->stream));
+            HIP_TRY(hipEventRecord(pb.done, f->stream));
+        }
         Batch b = make_batch(static_cast<const uint8_t*>(f->dkeys.p),
                              offsets ? static_cast<const uint64_t*>(f->doffs.p) : nullptr, key_len, cn);
         int rc = op(b, i0);

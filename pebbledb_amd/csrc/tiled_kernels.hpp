@@ -45,11 +45,11 @@ struct TileMap {
 };
 
 struct PartGeom {
-    uint32_t G;     // partition workgroups
-    uint32_t cap;   // region capacity in entries (multiple of 32)
-    uint32_t kps;   // keys per sub-chunk (multiple of 64, <= 2048 for probes)
-    uint32_t nsub;  // sub-chunks per workgroup
-    uint64_t kpw;   // keys per workgroup (= nsub * kps)
+    uint32_t G;        // partition workgroups
+    uint32_t cap;      // region capacity in entries (multiple of 32)
+    uint32_t kps;      // keys per sub-chunk (kpt * 1024; <= 4096 for probes)
+    uint32_t nsub;     // sub-chunks per workgroup
+    uint64_t kpw;      // keys per workgroup (= nsub * kps)
 };
 
 constexpr uint32_t kSlotShift = 20;   // probe entry = slot-in-sub-chunk << 20 | position in tile
@@ -71,6 +71,22 @@ __device__ __forceinline__ uint64_t tile_word0(uint32_t t, const TileMap& tm) {
     if (tm.cspace && p0 >= (1ull << 31)) w += tm.delta_words;
     return w;
 }
+
+// Diagnostic phase stamps (tools/microbench/part_phases.hip builds with PBF_STAMPS; the product
+// build compiles them away).  Workgroup 0, wave 0, lane 0 records s_memtime per phase.
+#ifdef PBF_STAMPS
+__device__ unsigned long long* g_stamps;
+#define PBF_STAMP(slot)                                                                         \
+    do {                                                                                        \
+        __builtin_amdgcn_sched_barrier(0);                                                      \
+        unsigned long long t_;                                                                  \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");              \
+        if (blockIdx.x == 0 && threadIdx.x == 0) g_stamps[(slot)] += t_;                        \
+        __builtin_amdgcn_sched_barrier(0);                                                      \
+    } while (0)
+#else
+#define PBF_STAMP(slot) do {} while (0)
+#endif
 
 // Barrier for LDS hand-offs only: waits for this wave's LDS/scalar operations, not for its
 // global stores (which __syncthreads' workgroup-release fence would drain every time).
@@ -130,14 +146,13 @@ __device__ __forceinline__ uint32_t bucket_of(const uint32_t* a, uint32_t B, uin
 // One 1024-thread workgroup per CU.  Each thread keeps up to KPT keys' KMAX (position, rank)
 // pairs in registers between the counting pass and the LDS placement, so every key is hashed
 // once; pg.kps = kpt_eff * 1024 keys per sub-chunk (kpt_eff <= KPT chosen by the host so the
-// stage fits LDS).  Each tile's run of a sub-chunk is written by one wave as one contiguous
-// store (runs of ~E/B entries), which keeps HBM write requests whole.
+// stage fits LDS).
 constexpr int kPartThreads = 1024;
 __host__ __device__ constexpr int part_kpt(int kmax, int km, bool probe) {
     // sized so every (KMAX, key mode) variant stays within 128 VGPRs without spilling
     if (km == kFixed16) {
-        if (kmax <= 4) return probe ? 4 : 6;
-        if (kmax <= 8) return probe ? 3 : 4;
+        if (kmax <= 4) return 4;
+        if (kmax <= 8) return 3;
         return kmax <= 16 ? 2 : 1;
     }
     return kmax <= 4 ? 4 : (kmax <= 8 ? 2 : 1);
@@ -153,7 +168,6 @@ __global__ void __launch_bounds__(kPartThreads) k_part(KeySet ks, uint64_t n, in
     extern __shared__ uint32_t smem[];
     const uint32_t B = tm.nbuckets;
     const uint32_t tid = threadIdx.x, nt = blockDim.x;
-    const uint32_t lane = tid & 63, wave = tid >> 6, nwaves = nt >> 6;
     const uint32_t kpt = pg.kps / nt;  // <= KPT
     const uint32_t g = blockIdx.x;
     uint32_t* cursor = smem;           // B: entries routed to (g, b) so far
@@ -161,6 +175,7 @@ __global__ void __launch_bounds__(kPartThreads) k_part(KeySet ks, uint64_t n, in
     uint32_t* lbase = cnt + B;         // B+1
     uint32_t* ws = lbase + B + 1;      // 16
     uint32_t* stage = ws + 16;         // kps * k
+    uint16_t* bkt = reinterpret_cast<uint16_t*>(stage + pg.kps * uint32_t(k));  // kps * k (probes)
     const uint32_t lmask = (1u << tm.tb) - 1u;
     for (uint32_t b = tid; b < B; b += nt) cursor[b] = 0;
     const uint64_t k0 = uint64_t(g) * pg.kpw;
@@ -180,9 +195,14 @@ __global__ void __launch_bounds__(kPartThreads) k_part(KeySet ks, uint64_t n, in
     uint32_t j = 0;
     for (uint64_t s0 = k0; s0 < k1; s0 += pg.kps, ++j) {
         const uint64_t s1 = min(k1, s0 + pg.kps);
+        PBF_STAMP(0);
         for (uint32_t b = tid; b < B; b += nt) cnt[b] = 0;
         lds_barrier();
+        PBF_STAMP(1);
+        // (initialised so no value stays live across the sub-chunk loop's back-edge)
         uint32_t pos[KPT * KMAX], rk[KPT * KMAX];
+#pragma unroll
+        for (int e = 0; e < KPT * KMAX; ++e) pos[e] = rk[e] = 0;
 #pragma unroll
         for (int u = 0; u < KPT; ++u) {
             const uint64_t i = s0 + u * nt + tid;
@@ -198,12 +218,15 @@ __global__ void __launch_bounds__(kPartThreads) k_part(KeySet ks, uint64_t n, in
                     hash_key<KMAX, KM>(ks, i, k, emit);
             }
         }
+        PBF_STAMP(2);
         lds_barrier();
+        PBF_STAMP(3);
         if constexpr (PROBE) {
             uint32_t* sc = subcnt + (uint64_t(g) * pg.nsub + j) * B;
             for (uint32_t b = tid; b < B; b += nt) sc[b] = cnt[b];
         }
         block_exclusive_scan(cnt, lbase, B, ws);
+        PBF_STAMP(4);
 #pragma unroll
         for (int u = 0; u < KPT; ++u) {
             const uint32_t slot_key = u * nt + tid;
@@ -214,33 +237,51 @@ __global__ void __launch_bounds__(kPartThreads) k_part(KeySet ks, uint64_t n, in
                         const uint32_t p = pos[u * KMAX + s];
                         const uint32_t slot = lbase[p >> tm.tb] + rk[u * KMAX + s];
                         stage[slot] = PROBE ? ((slot_key << kSlotShift) | (p & lmask)) : p;
+                        if constexpr (PROBE) bkt[slot] = uint16_t(p >> tm.tb);
+                    }
+                }
+            }
+        }
+        for (uint32_t b = tid; b < B; b += nt) cursor[b] -= lbase[b];
+        lds_barrier();
+        PBF_STAMP(5);
+        if (s0 + pg.kps < k1) load_keys(s0 + pg.kps);
+        // Lane-parallel write-out: entry e of the sorted stage goes to position
+        // cursor[b] + (e - lbase[b]) of region (g, b) (cursor pre-biased by -lbase below).
+        // Eight entries per thread per batch, loads unconditional, so each thread has eight
+        // independent LDS → store chains in flight.  Positions >= cap overflow.
+        const uint32_t tot = lbase[B];
+        constexpr int UW = 8;
+        for (uint32_t e0 = tid; e0 < tot; e0 += nt * UW) {
+            uint32_t v[UW], b[UW];
+#pragma unroll
+            for (int u = 0; u < UW; ++u) {
+                const uint32_t e = min(e0 + u * nt, tot - 1);
+                v[u] = stage[e];
+                b[u] = PROBE ? uint32_t(bkt[e]) : (v[u] >> tm.tb);
+            }
+#pragma unroll
+            for (int u = 0; u < UW; ++u) {
+                const uint32_t e = e0 + u * nt;
+                const uint32_t r = cursor[b[u]] + e;
+                if (e < tot) {
+                    if (r < pg.cap) {
+                        regions[(uint64_t(g) * B + b[u]) * pg.cap + r] = v[u];
+                    } else if constexpr (PROBE) {
+                        const uint64_t bit = pos_to_bit((b[u] << tm.tb) | (v[u] & lmask), tm);
+                        if (!((bitmap[bit >> 5] >> (bit & 31)) & 1u)) {
+                            const uint64_t key = s0 + (v[u] >> kSlotShift);
+                            atomicOr(neg + (key >> 5), 1u << (key & 31));
+                        }
+                    } else {
+                        ovf[atomicAdd(ovf_count, 1u)] = v[u];
                     }
                 }
             }
         }
         lds_barrier();
-        if (s0 + pg.kps < k1) load_keys(s0 + pg.kps);
-        // one wave per tile run: contiguous stores into region (g, b)
-        for (uint32_t b = wave; b < B; b += nwaves) {
-            const uint32_t lb = lbase[b], len = lbase[b + 1] - lb, cur = cursor[b];
-            uint32_t* dst = regions + (uint64_t(g) * B + b) * pg.cap;
-            for (uint32_t i = lane; i < len; i += 64) {
-                const uint32_t v = stage[lb + i];
-                const uint32_t r = cur + i;
-                if (r < pg.cap) {
-                    dst[r] = v;
-                } else if constexpr (PROBE) {
-                    const uint64_t bit = pos_to_bit((b << tm.tb) | (v & lmask), tm);
-                    if (!((bitmap[bit >> 5] >> (bit & 31)) & 1u)) {
-                        const uint64_t key = s0 + (v >> kSlotShift);
-                        atomicOr(neg + (key >> 5), 1u << (key & 31));
-                    }
-                } else {
-                    ovf[atomicAdd(ovf_count, 1u)] = v;
-                }
-            }
-            if (lane == 0) cursor[b] = cur + len;
-        }
+        for (uint32_t b = tid; b < B; b += nt) cursor[b] += lbase[b + 1];
+        PBF_STAMP(6);
     }
     lds_barrier();
     for (uint32_t b = tid; b < B; b += nt) fill[uint64_t(b) * pg.G + g] = min(cursor[b], pg.cap);
@@ -314,7 +355,6 @@ __global__ void __launch_bounds__(1024) k_tile_build(TileMap tm, PartGeom pg, co
     lds_barrier();
     const uint32_t lane = tid & 63, wave = tid >> 6, nwaves = nt >> 6;
     const uint32_t lmask = (1u << tm.tb) - 1u;
-    const uint32_t lc = min(lane, cap / 4 - 1);  // unconditional loads stay inside the region
     constexpr int U = 4;
     for (uint32_t g0 = wave; g0 < G; g0 += nwaves * U) {
         uint4 v[U];
@@ -323,6 +363,8 @@ __global__ void __launch_bounds__(1024) k_tile_build(TileMap tm, PartGeom pg, co
         for (int u = 0; u < U; ++u) {
             const uint32_t q = g0 + u * nwaves;
             f[u] = q < G ? fills[q] : 0u;
+            // unconditional loads, clamped to the filled part (idle lanes re-read its last line)
+            const uint32_t lc = min(lane, (max(f[u], 1u) - 1) >> 2);
             v[u] = reinterpret_cast<const uint4*>(regions + (uint64_t(min(q, G - 1)) * B + b) * cap)[lc];
         }
 #pragma unroll
@@ -422,71 +464,105 @@ __global__ void __launch_bounds__(1024) k_tile_probe(TileMap tm, PartGeom pg, co
     }
 }
 
-// Workgroup g replays its sub-chunks (same geometry as k_part<probe>).  One wave per tile reads
-// the sub-chunk's in-region run of (g, b) and its result bits, and clears the flag of every key
-// with a 0 bit; then the sub-chunk's keys are balloted into hit-mask words.
+// Workgroup g owns keys [g*kpw, (g+1)*kpw) and regions (g, 0..B-1).  It reads each region once,
+// contiguously, with its result bits; an entry's sub-chunk j follows from the region's run
+// boundaries (prefix over j of the in-region counts, from subcnt), and its key is
+// g*kpw + j*kps + slot.  A 0 result bit clears the key's bit in an LDS bitmap of the
+// workgroup's keys, which is finally written out as hit-mask words.
+//   LDS: pref[B][nsub+1] (u16 run boundaries, region-relative), kbits[kpw/32].
 __global__ void __launch_bounds__(1024) k_gather(TileMap tm, PartGeom pg, uint64_t n,
                                                  const uint32_t* __restrict__ regions, const uint32_t* __restrict__ R,
                                                  const uint32_t* __restrict__ subcnt, const uint32_t* __restrict__ neg,
                                                  uint8_t* __restrict__ hitmask) {
     extern __shared__ uint32_t smem[];
-    const uint32_t B = tm.nbuckets, cap = pg.cap, wpr = cap / 32;
+    const uint32_t B = tm.nbuckets, cap = pg.cap, wpr = cap / 32, nsub = pg.nsub;
     const uint32_t tid = threadIdx.x, nt = blockDim.x;
     const uint32_t lane = tid & 63, wave = tid >> 6, nwaves = nt >> 6;
     const uint32_t g = blockIdx.x;
-    uint32_t* cursor = smem;         // B
-    uint32_t* cnt = cursor + B;      // B
-    uint32_t* flags = cnt + B;       // kps
-    for (uint32_t b = tid; b < B; b += nt) cursor[b] = 0;
     const uint64_t k0 = uint64_t(g) * pg.kpw;
     const uint64_t k1 = min(n, k0 + pg.kpw);
-    uint32_t j = 0;
-    for (uint64_t s0 = k0; s0 < k1; s0 += pg.kps, ++j) {
-        const uint32_t nk = uint32_t(min<uint64_t>(k1 - s0, pg.kps));
-        const uint32_t* sc = subcnt + (uint64_t(g) * pg.nsub + j) * B;
-        lds_barrier();
-        for (uint32_t b = tid; b < B; b += nt) cnt[b] = sc[b];
-        for (uint32_t s = tid; s < pg.kps; s += nt) {
-            const uint64_t key = s0 + s;
-            flags[s] = (s < nk && !((neg[key >> 5] >> (key & 31)) & 1u)) ? 1u : 0u;
+    const uint32_t nkeys = uint32_t(k1 - k0);
+    const uint32_t kw = uint32_t((pg.kpw + 31) / 32);
+    uint32_t* kbits = smem;                                    // kw words
+    uint16_t* pref = reinterpret_cast<uint16_t*>(kbits + kw);  // B * (nsub + 1)
+    const uint32_t ps = nsub + 1;
+    // key bits: 1 for this workgroup's keys not already refuted by an overflow entry
+    for (uint32_t w = tid; w < kw; w += nt) {
+        const uint32_t key0 = w * 32;
+        uint32_t m = key0 >= nkeys ? 0u : (nkeys - key0 >= 32 ? ~0u : ((1u << (nkeys - key0)) - 1u));
+        if (m) {
+            const uint64_t gk = k0 + key0;  // neg is indexed by batch key; k0 is a multiple of 64
+            m &= ~neg[gk >> 5];
         }
-        lds_barrier();
-        constexpr int U = 4;
-        for (uint32_t b0 = wave; b0 < B; b0 += nwaves * U) {
-            uint32_t v[U], rw[U], len[U], r[U];
+        kbits[w] = m;
+    }
+    // run boundaries per tile: pref[b][j] = in-region entries of (g, b) before sub-chunk j
+    const uint32_t* sc = subcnt + uint64_t(g) * nsub * B;
+    for (uint32_t b = tid; b < B; b += nt) {
+        uint32_t run = 0;
+        pref[b * ps] = 0;
+        for (uint32_t j0 = 0; j0 < nsub; j0 += 8) {
+            uint32_t c[8];
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const uint32_t b = min(b0 + u * nwaves, B - 1);
-                const uint32_t cur = cursor[b];
-                len[u] = (b0 + u * nwaves < B && cur < cap) ? min(cnt[b], cap - cur) : 0u;
-                r[u] = min(cur + lane, cap - 1);  // unconditional loads stay inside the region
-                const uint64_t reg = uint64_t(g) * B + b;
-                v[u] = regions[reg * cap + r[u]];
-                rw[u] = R[reg * wpr + (r[u] >> 5)];
-            }
+            for (int u = 0; u < 8; ++u) c[u] = j0 + u < nsub ? sc[uint64_t(j0 + u) * B + b] : 0u;
 #pragma unroll
-            for (int u = 0; u < U; ++u)
-                if (lane < len[u] && !((rw[u] >> (r[u] & 31)) & 1u)) flags[(v[u] >> kSlotShift) & kSlotMask] = 0u;
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const uint32_t b = b0 + u * nwaves;
-                if (b < B) {
-                    const uint32_t cur = cursor[b];
-                    const uint64_t reg = uint64_t(g) * B + b;
-                    for (uint32_t i = 64 + lane; i < len[u]; i += 64) {  // runs longer than a wave
-                        const uint32_t rr = cur + i;
-                        if (!((R[reg * wpr + (rr >> 5)] >> (rr & 31)) & 1u))
-                            flags[(regions[reg * cap + rr] >> kSlotShift) & kSlotMask] = 0u;
-                    }
-                    if (lane == 0) cursor[b] = cur + cnt[b];
+            for (int u = 0; u < 8; ++u) {
+                if (j0 + u < nsub) {
+                    run = min(run + c[u], cap);
+                    pref[b * ps + j0 + u + 1] = uint16_t(run);
                 }
             }
         }
-        lds_barrier();
-        for (uint32_t s = tid; s < ((nk + 63) & ~63u); s += nt) {
-            const unsigned long long bal = __ballot(s < nk && flags[s] != 0u);
-            if ((s & 63) == 0) store_hit_word(hitmask, n, s0 + s, bal);
+    }
+    lds_barrier();
+    // one wave per region; U 64-entry windows (from different regions) in flight per wave
+    constexpr int U = 4;
+    for (uint32_t b0 = wave; b0 < B; b0 += nwaves * U) {
+        uint32_t fillb[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) fillb[u] = b0 + u * nwaves < B ? uint32_t(pref[(b0 + u * nwaves) * ps + nsub]) : 0u;
+        uint32_t maxf = 0;
+#pragma unroll
+        for (int u = 0; u < U; ++u) maxf = max(maxf, fillb[u]);
+        for (uint32_t r0 = 0; r0 < maxf; r0 += 64) {
+            uint32_t v[U], rw[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t b = min(b0 + u * nwaves, B - 1);
+                const uint32_t r = min(r0 + lane, max(fillb[u], 1u) - 1);
+                const uint64_t reg = uint64_t(g) * B + b;
+                v[u] = regions[reg * cap + r];
+                rw[u] = R[reg * wpr + (r >> 5)];
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t b = b0 + u * nwaves;
+                const uint32_t r = r0 + lane;
+                if (b < B && r < fillb[u] && !((rw[u] >> (r & 31)) & 1u)) {
+                    // sub-chunk of position r: the last j with pref[b][j] <= r
+                    const uint16_t* pb = pref + b * ps;
+                    uint32_t lo = 0, len = nsub;
+                    while (len > 1) {
+                        const uint32_t half = len >> 1;
+                        if (pb[lo + half] <= r) lo += half;
+                        len -= half;
+                    }
+                    const uint32_t key = lo * pg.kps + ((v[u] >> kSlotShift) & kSlotMask);
+                    atomicAnd(kbits + (key >> 5), ~(1u << (key & 31)));
+                }
+            }
         }
+    }
+    lds_barrier();
+    // hit-mask words for keys [k0, k1): k0 is a multiple of 64
+    for (uint32_t w = tid; w * 32 < nkeys; w += nt) {
+        const uint64_t key0 = k0 + uint64_t(w) * 32;
+        const uint32_t bits = kbits[w];
+        const uint64_t nb = min<uint64_t>(4, (n - key0 + 7) / 8);
+        if (nb == 4 && (reinterpret_cast<uintptr_t>(hitmask + key0 / 8) & 3) == 0)
+            *reinterpret_cast<uint32_t*>(hitmask + key0 / 8) = bits;
+        else
+            for (uint64_t q = 0; q < nb; ++q) hitmask[key0 / 8 + q] = uint8_t(bits >> (8 * q));
     }
 }
 

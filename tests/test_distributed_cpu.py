@@ -1,0 +1,100 @@
+"""Multi-GPU sharding logic on CPU: gloo, world_size 2 (the N>1 path of bench.py and the
+config-4/5 placement).  The per-rank filter work is done by the CPU oracle here (tests may use
+it as the checker); what is under test is the partition, the disjointness and the
+max-over-ranks / gather bookkeeping."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from pebbledb_amd.shard import candidate_order, filters_for_rank, gather_hitmasks, key_range, owner_of
+
+
+def test_filters_for_rank_partition():
+    for n in (1, 7, 8, 9, 64):
+        for w in (1, 2, 3, 4, 8):
+            got = [filters_for_rank(n, w, r) for r in range(w)]
+            flat = [f for fs in got for f in fs]
+            assert flat == list(range(n))
+            sizes = [len(fs) for fs in got]
+            assert max(sizes) - min(sizes) <= 1
+            for r, fs in enumerate(got):
+                assert all(owner_of(f, n, w) == r for f in fs)
+    assert filters_for_rank(8, 8, 3) == [3]
+    assert filters_for_rank(8, 2, 1) == [4, 5, 6, 7]
+    with pytest.raises(ValueError):
+        filters_for_rank(8, 2, 2)
+
+
+def test_key_ranges_disjoint():
+    rs = [key_range(f, 125) for f in range(8)]
+    assert rs[0] == (0, 125) and rs[-1] == (875, 1000)
+    assert all(a[1] == b[0] for a, b in zip(rs, rs[1:]))
+
+
+def test_candidate_order_matches_lsm_get():
+    # lsm_storage.py:164-179: L0 newest first, then level by level
+    assert candidate_order(np.array([0, 1, 1]), [np.array([1, 0]), np.array([0, 1])]) == [1, 2, 3, 6]
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import torch
+    from oracle.oracle import COracle
+    from pebbledb_amd.keys import PackedKeys, splitmix_hex_keys
+    o = COracle()
+    n_filters, kpf, nb, k = 8, 3000, 4096, 6
+    mine = filters_for_rank(n_filters, world, rank)
+    probe = PackedKeys.fixed(splitmix_hex_keys(77, 0, n_filters * kpf + 5000))
+    local = {}
+    for f in mine:
+        a, b = key_range(f, kpf)
+        bm = o.build(nb, k, PackedKeys.fixed(splitmix_hex_keys(77, a, b - a)))
+        local[f] = o.probe(bm, k, probe)
+    # gather every rank's hit masks on every rank (host-side bookkeeping, not the data path)
+    objs = [None] * world
+    dist.all_gather_object(objs, local)
+    merged = {}
+    for d in objs:
+        merged.update(d)
+    t = torch.tensor([float(rank + 1)])
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    q.put((rank, sorted(merged), float(t.item()), {f: v.tobytes() for f, v in merged.items()}))
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_sharded_filters_equal_single_process():
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, fids, tmax, masks in res:
+        assert fids == list(range(8)) and tmax == 2.0
+    # single-process reference
+    from oracle.oracle import COracle
+    from pebbledb_amd.keys import PackedKeys, splitmix_hex_keys
+    o = COracle()
+    probe = PackedKeys.fixed(splitmix_hex_keys(77, 0, 8 * 3000 + 5000))
+    masks = res[0][3]
+    mat = gather_hitmasks({f: np.frombuffer(m, np.uint8) for f, m in masks.items()}, 8, probe.n)
+    for f in range(8):
+        a, b = key_range(f, 3000)
+        bm = o.build(4096, 6, PackedKeys.fixed(splitmix_hex_keys(77, a, b - a)))
+        assert np.array_equal(np.frombuffer(masks[f], np.uint8), o.probe(bm, 6, probe))
+        assert mat[f, a:b].all()  # members of filter f hit filter f

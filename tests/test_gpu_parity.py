@@ -326,3 +326,22 @@ def test_small_host_stage_chunks(oracle, monkeypatch):
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=600,
                        cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
+
+
+def test_sstable_section_roundtrip_golden():
+    """encode_sstable / decode_bloom_section against the reference's own SSTable bytes
+    (src/sstable.py:80-100, via tests/golden/sstable_section.json)."""
+    from pebbledb_amd.sstable_bloom import decode_bloom_section, encode_sstable
+    g = load_golden("sstable_section.json")
+    bf = BloomFilter.build_from_keys_and_fp_rate(g["keys"], g["fp_rate"])
+    out = encode_sstable(bytes.fromhex(g["data_hex"]), bytes.fromhex(g["meta_hex"]), bf)
+    assert bytes(out) == bytes.fromhex(g["sstable_hex"])
+    back = decode_bloom_section(out)
+    assert back == bf and back.nb_bytes == bf.nb_bytes
+    assert all(back.may_contain(k) for k in g["keys"])
+    # a big filter through the same path (bitmap copied device → file buffer → device)
+    keys = PackedKeys.fixed(splitmix_hex_keys(3, 0, 200000))
+    big = BloomFilter.build_from_keys_and_fp_rate(keys, 0.001)
+    blob = encode_sstable(b"x" * 1000, b"m" * 77, big)
+    again = decode_bloom_section(blob)
+    assert again.bitmap() == big.bitmap() and again.nb_hash_functions == big.nb_hash_functions

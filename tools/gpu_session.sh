@@ -22,6 +22,7 @@ for step in "$@"; do
     pytest) run pytest 1200 python -m pytest tests -m gpu -q -rf ;;
     bench) run bench 600 python bench.py --steps 20 --warmup 5 ;;
     bench_atomic) run bench_atomic 600 python bench.py --steps 10 --warmup 3 --build-mode 1 --no-cpu-baseline ;;
+    bench_tt) run bench_tt 300 python bench.py --steps 20 --warmup 5 --build-mode 2 --probe-mode 2 --no-cpu-baseline --no-host-inclusive ;;
     bench_modes) for bm in 1 2; do for pm in 1 2; do run bench_b${bm}_p${pm} 300 python bench.py --steps 20 --warmup 5 --build-mode $bm --probe-mode $pm --no-cpu-baseline; done; done ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
     probe_s1) for s1 in 1 2 3 6; do PBF_PROBE_S1=$s1 run probe_s1_$s1 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline; done ;;
@@ -30,6 +31,13 @@ for step in "$@"; do
          run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline
          run pmc_tcc 600 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum --output-format csv -d gpurun_out/pmc_tcc -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
     micro) run micro 300 tools/microbench/lds_rates ;;
+    phases) run phases 300 tools/microbench/part_phases ;;
+    gapdiag) run native0 120 tools/microbench/pipeline_bench 50 0
+             run native1 120 tools/microbench/pipeline_bench 50 1
+             run native2 120 tools/microbench/pipeline_bench 50 2
+             run native0b 120 tools/microbench/pipeline_bench 200 0
+             run py_ev 300 python bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-host-inclusive
+             run py_noev 300 python bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-host-inclusive --no-events ;;
     pmcall) run pmcall 2400 tools/pmc_passes.sh gpurun_out/pmcall ;;
     pmcdirect) run pmcdirect 2400 tools/pmc_passes.sh gpurun_out/pmcdirect --probe-mode 1 ;;
     diag) run diag_a 300 python bench.py --steps 20 --warmup 5 --build-mode 2 --probe-mode 1 --no-cpu-baseline
