@@ -19,12 +19,13 @@ run() {  # name seconds cmd...
 for step in "$@"; do
   case $step in
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    pytest) run pytest 1200 python -m pytest tests -m gpu -q -rf ;;
+    pytest) run pytest 900 python -u -m pytest tests -m gpu -x -v -rf --timeout 120 --timeout-method thread ;;
     bench) run bench 600 python bench.py --steps 20 --warmup 5 ;;
     bench_atomic) run bench_atomic 600 python bench.py --steps 10 --warmup 3 --build-mode 1 --no-cpu-baseline ;;
     bench_tt) run bench_tt 300 python bench.py --steps 20 --warmup 5 --build-mode 2 --probe-mode 2 --no-cpu-baseline --no-host-inclusive ;;
     bench_modes) for bm in 1 2; do for pm in 1 2; do run bench_b${bm}_p${pm} 300 python bench.py --steps 20 --warmup 5 --build-mode $bm --probe-mode $pm --no-cpu-baseline; done; done ;;
-    prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
+    prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline
+          python tools/prof_summary.py gpurun_out/prof > gpurun_out/prof_summary.txt 2>&1 || true ;;
     probe_s1) for s1 in 1 2 3 6; do PBF_PROBE_S1=$s1 run probe_s1_$s1 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline; done ;;
     pmc) run counters 120 rocprofv3 -L
          run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline
