@@ -224,28 +224,34 @@ def main():
         if ev is not None:
             ev[2].record(stream)
 
+    events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    span = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    # warm-up right before the timed region: the GPU is never idle long before t0 (a queue left
+    # idle for ~100 ms was seen to start its next submission up to ~20 ms late)
     for _ in range(args.warmup):
         step()
     bf.sync()
-    # correctness guard on the measured data: every member must hit
-    hm = hitmask.cpu().numpy()
-    members_ok = bool((np.unpackbits(hm, bitorder="little")[:n] == 1).all())
-    fp = int(np.unpackbits(hm, bitorder="little")[n:2 * n].sum())
-
-    events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     bf.sync()
     t0 = time.perf_counter()
+    span[0].record(stream)
     for s in range(args.steps):
         step(None if args.no_events else events[s])
         if args.sync_each_step:
             bf.sync()
+    span[1].record(stream)
     t_enq = time.perf_counter()
     bf.sync()
+    t_done = time.perf_counter()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
+    gpu_span_ms = span[0].elapsed_time(span[1])
+    # correctness guard on the measured data (the last step's hit mask): every member must hit
+    hm = hitmask.cpu().numpy()
+    members_ok = bool((np.unpackbits(hm, bitorder="little")[:n] == 1).all())
+    fp = int(np.unpackbits(hm, bitorder="little")[n:2 * n].sum())
     if world > 1:
         dist.barrier()
     elapsed = t1 - t0
@@ -302,6 +308,8 @@ def main():
                                    f"; one filter per GPU", "n_build": n, "n_probe": 2 * n, "nb_bytes": nb_bytes, "k": k,
                        "keys_per_step_per_gpu": 3 * n, "parallelism": f"filter-per-gpu x{world}"},
             "host_enqueue_ms_per_step": round((t_enq - t0) / args.steps * 1e3, 4),
+            "gpu_span_ms_per_step": round(gpu_span_ms / args.steps, 4),
+            "host_wait_ms": {"stream_done": round((t_done - t_enq) * 1e3, 3), "device_sync": round((t1 - t_done) * 1e3, 3)},
             "build_ms": round(build_ms, 4),
             "probe_ms": round(probe_ms, 4),
             "build_Mkeys_s_per_gpu": round(n / build_ms / 1e3, 1),

@@ -23,6 +23,7 @@
 #include "../../include/pebblebloom.h"
 #include "bloom_kernels.hpp"
 #include "tiled_kernels.hpp"
+#include "ring_kernels.hpp"
 
 using namespace pbf;
 
@@ -259,12 +260,60 @@ int run_atomic(pbf_filter_t* f, const Batch& b) {
 struct PartPlan {
     PartGeom pg;
     size_t lds_part;
+    size_t lds_gather;  // probes
 };
+
+// Partition strategy: PBF_PART=sort|ring forces one (tests, measurements); default auto.
+int part_override() {
+    static const int v = [] {
+        const char* e = std::getenv("PBF_PART");
+        if (!e) return 0;
+        if (!std::strcmp(e, "sort")) return 1;
+        if (!std::strcmp(e, "ring")) return 2;
+        return 0;
+    }();
+    return v;
+}
+
+// Ring partition (ring_kernels.hpp) when there are many tiles: a 1024-key sub-chunk then puts
+// only a few positions into each tile (<= GS/2 on average), which is what the ring's GS-entry
+// groups need, while the counting-sort partition's per-tile runs get too short to write well.
+// Ring of 32 entries (64-B groups) up to 1024 tiles, of 16 (32-B groups) up to 2048.
+uint32_t ring_entries(uint32_t B, uint32_t k, bool probe, uint32_t tb) {
+    if (probe && tb > kSlotShift) return 0;
+    const int ov = part_override();
+    if (ov == 1) return 0;
+    const uint32_t rc = B <= 1024 ? 32 : (B <= 2048 ? 16 : 0);
+    if (!rc) return 0;
+    if (ov == 2) return rc;
+    // mean positions per tile per sub-chunk = 1024*k/B <= GS/2 = rc/4
+    return uint64_t(kRingKeysPerSub) * k * 4 <= uint64_t(B) * rc ? rc : 0;
+}
+
+PartPlan plan_ring(uint32_t B, uint32_t k, uint64_t n, uint32_t rc) {
+    PartPlan pl{};
+    const uint64_t kps = kRingKeysPerSub;
+    const uint64_t G0 = std::min<uint64_t>(256, std::max<uint64_t>(1, (n + kps - 1) / kps));
+    uint64_t kpw = (n + G0 - 1) / G0;
+    kpw = ((kpw + kps - 1) / kps) * kps;
+    pl.pg.G = uint32_t(std::max<uint64_t>(1, (n + kpw - 1) / kpw));
+    pl.pg.kps = uint32_t(kps);
+    pl.pg.kpw = kpw;
+    pl.pg.nsub = uint32_t(kpw / kps);
+    pl.pg.nq = (pl.pg.nsub + 3) / 4;
+    pl.pg.ring = rc;
+    const double mu = double(kpw) * k / B;
+    const uint64_t cap = uint64_t(mu + 8.0 * std::sqrt(mu) + 32.0);
+    pl.pg.cap = uint32_t(((cap + 31) / 32) * 32);
+    pl.lds_part = size_t((2 * B + 16 * 128 + 3) & ~3u) * 4 + size_t(B) * rc * 4;
+    pl.lds_gather = size_t((kpw + 31) / 32) * 4 + size_t(B) * (pl.pg.nq + 1) * 2 + 16;
+    return pl;
+}
 
 PartPlan plan_partition(uint32_t B, uint32_t k, int km, uint64_t n, bool probe) {
     PartPlan pl{};
-    const size_t fixed = size_t(3 * B + 1 + 16) * 4;
     const size_t per_entry = probe ? 6 : 4;  // stage u32 (+ u16 tile id for probes)
+    const size_t fixed = size_t(3 * B + 1 + 16) * 4;
     // keys per thread per sub-chunk: as many as the registers (part_kpt) and the LDS allow
     uint64_t kpt = uint64_t(part_kpt(kmax_for(k), km, probe));
     while (kpt > 1 && fixed + kpt * kPartThreads * k * per_entry > 156 * 1024) --kpt;
@@ -281,14 +330,20 @@ PartPlan plan_partition(uint32_t B, uint32_t k, int km, uint64_t n, bool probe) 
     const double mu = double(kpw) * k / B;
     const uint64_t cap = uint64_t(mu + 8.0 * std::sqrt(mu) + 32.0);
     pl.pg.cap = uint32_t(((cap + 31) / 32) * 32);
+    pl.lds_gather = size_t((pl.pg.kpw + 31) / 32) * 4 + size_t(B) * (pl.pg.nsub + 1) * 2 + 16;
     return pl;
+}
+
+PartPlan plan_for(uint32_t B, uint32_t k, int km, uint64_t n, bool probe, uint32_t tb) {
+    const uint32_t rc = ring_entries(B, k, probe, tb);
+    return rc ? plan_ring(B, k, n, rc) : plan_partition(B, k, km, n, probe);
 }
 
 int run_tiled(pbf_filter_t* f, const Batch& b) {
     const TileMap& tm = f->tm;
     const uint32_t B = tm.nbuckets;
     const uint32_t k = f->k;
-    const PartPlan pl = plan_partition(B, k, b.km, b.n, false);
+    const PartPlan pl = plan_for(B, k, b.km, b.n, false, tm.tb);
     const PartGeom& pg = pl.pg;
     HIP_TRY(f->regions.ensure(size_t(pg.G) * B * pg.cap * 4));
     HIP_TRY(f->fill.ensure(size_t(pg.G) * B * 4));
@@ -303,7 +358,8 @@ int run_tiled(pbf_filter_t* f, const Batch& b) {
     hipError_t err = hipSuccess;
     dispatch(kmax_for(k), b.km, [&](auto KMAX, auto KM) {
         if constexpr (decltype(KMAX)::value > 0) {  // tiled path only for k <= 32
-            auto kern = k_part<decltype(KMAX)::value, decltype(KM)::value, false>;
+            auto kern = pg.ring ? k_part_ring<decltype(KMAX)::value, decltype(KM)::value, false>
+                                : k_part<decltype(KMAX)::value, decltype(KM)::value, false>;
             err = allow_lds(kern, pl.lds_part);
             if (err == hipSuccess)
                 kern<<<pg.G, kPartThreads, pl.lds_part, s>>>(b.ks, b.n, int(k), tm, pg, regions, fill, nullptr, ovf,
@@ -326,11 +382,12 @@ int run_tiled_probe(pbf_filter_t* f, const Batch& b, uint8_t* hitmask) {
     const TileMap& tm = f->tm;
     const uint32_t B = tm.nbuckets;
     const uint32_t k = f->k;
-    const PartPlan pl = plan_partition(B, k, b.km, b.n, true);
+    const PartPlan pl = plan_for(B, k, b.km, b.n, true, tm.tb);
     const PartGeom& pg = pl.pg;
     HIP_TRY(f->regions.ensure(size_t(pg.G) * B * pg.cap * 4));
     HIP_TRY(f->fill.ensure(size_t(pg.G) * B * 4));
-    HIP_TRY(f->subcnt.ensure(size_t(pg.G) * pg.nsub * B * 4));
+    // sort partition: per-sub-chunk tile counts; ring partition: cumulative counts per 4 sub-chunks
+    HIP_TRY(f->subcnt.ensure(pg.ring ? size_t(pg.G) * B * (pg.nq + 1) * 4 : size_t(pg.G) * pg.nsub * B * 4));
     HIP_TRY(f->rbits.ensure(size_t(pg.G) * B * (pg.cap / 32) * 4));
     const size_t neg_bytes = ((b.n + 31) / 32) * 4;
     HIP_TRY(f->neg.ensure(neg_bytes));
@@ -344,7 +401,8 @@ int run_tiled_probe(pbf_filter_t* f, const Batch& b, uint8_t* hitmask) {
     hipError_t err = hipSuccess;
     dispatch(kmax_for(k), b.km, [&](auto KMAX, auto KM) {
         if constexpr (decltype(KMAX)::value > 0) {
-            auto kern = k_part<decltype(KMAX)::value, decltype(KM)::value, true>;
+            auto kern = pg.ring ? k_part_ring<decltype(KMAX)::value, decltype(KM)::value, true>
+                                : k_part<decltype(KMAX)::value, decltype(KM)::value, true>;
             err = allow_lds(kern, pl.lds_part);
             if (err == hipSuccess)
                 kern<<<pg.G, kPartThreads, pl.lds_part, s>>>(b.ks, b.n, int(k), tm, pg, regions, fill, subcnt, nullptr,
@@ -360,15 +418,24 @@ int run_tiled_probe(pbf_filter_t* f, const Batch& b, uint8_t* hitmask) {
     HIP_TRY(allow_lds(k_tile_probe, lds_tile));
     k_tile_probe<<<B, 1024, lds_tile, s>>>(tm, pg, regions, fill, f->bitmap, R, expand);
     CHECK_LAUNCH();
-    const size_t lds_gather = size_t((pg.kpw + 31) / 32) * 4 + size_t(B) * (pg.nsub + 1) * 2 + 16;
-    HIP_TRY(allow_lds(k_gather, lds_gather));
-    k_gather<<<pg.G, 1024, lds_gather, s>>>(tm, pg, b.n, regions, R, subcnt, neg, hitmask);
+    if (pg.ring) {
+        HIP_TRY(allow_lds(k_gather_ring, pl.lds_gather));
+        k_gather_ring<<<pg.G, 1024, pl.lds_gather, s>>>(tm, pg, b.n, regions, R, fill, subcnt, neg, hitmask);
+    } else {
+        HIP_TRY(allow_lds(k_gather, pl.lds_gather));
+        k_gather<<<pg.G, 1024, pl.lds_gather, s>>>(tm, pg, b.n, regions, R, subcnt, neg, hitmask);
+    }
     CHECK_LAUNCH();
     return PBF_OK;
 }
 
+// The partition pass needs its tile counters plus a stage of one key per thread in LDS.
+bool part_fits(uint32_t B, uint32_t k, bool probe) {
+    return size_t(3 * B + 17) * 4 + size_t(kPartThreads) * k * (probe ? 6 : 4) <= 156 * 1024;
+}
+
 bool want_tiled(pbf_filter_t* f, uint64_t n) {
-    if (!f->tiled_ok || f->k == 0 || f->k > 32) return false;
+    if (!f->tiled_ok || f->k == 0 || f->k > 32 || !part_fits(f->tm.nbuckets, f->k, false)) return false;
     if (f->mode == PBF_BUILD_TILED) return true;
     if (f->mode == PBF_BUILD_ATOMIC) return false;
     const uint64_t npos = n * f->k;
@@ -379,7 +446,8 @@ bool want_tiled(pbf_filter_t* f, uint64_t n) {
 }
 
 bool want_tiled_probe(pbf_filter_t* f, uint64_t n) {
-    if (!f->tiled_ok || f->k == 0 || f->k > 32 || f->tm.tb > kSlotShift) return false;
+    if (!f->tiled_ok || f->k == 0 || f->k > 32 || f->tm.tb > kSlotShift || !part_fits(f->tm.nbuckets, f->k, true))
+        return false;
     if (f->probe_mode == PBF_PROBE_TILED) return true;
     if (f->probe_mode == PBF_PROBE_DIRECT) return false;
     // direct: ~1..k random 64-B requests per key, cheap while the bitmap stays in one XCD's
@@ -394,9 +462,8 @@ uint64_t tiled_probe_batch(pbf_filter_t* f, int km) {
     const uint32_t B = f->tm.nbuckets, k = f->k;
     uint64_t n = std::max<uint64_t>(64, (kMaxPositions / k) & ~uint64_t(63));
     for (;;) {
-        const PartPlan pl = plan_partition(B, k, km, n, true);
-        const size_t lds = size_t((pl.pg.kpw + 31) / 32) * 4 + size_t(B) * (pl.pg.nsub + 1) * 2 + 16;
-        if ((lds <= 156 * 1024 && pl.pg.cap <= 65535) || n <= 64 * 1024) return n;
+        const PartPlan pl = plan_for(B, k, km, n, true, f->tm.tb);
+        if ((pl.lds_gather <= 156 * 1024 && pl.pg.cap <= 65535) || n <= 64 * 1024) return n;
         n = std::max<uint64_t>(64 * 1024, (n / 2) & ~uint64_t(63));
     }
 }
@@ -816,7 +883,13 @@ int pbf_popcount(pbf_filter_t* f, uint64_t* out) {
 int pbf_sync(pbf_filter_t* f) {
     int rc = enter(f);
     if (rc) return rc;
-    HIP_TRY(hipStreamSynchronize(f->stream));
+    // Spin on the stream instead of a blocking wait: the caller is about to use the results,
+    // and a blocking synchronise can add milliseconds of wake-up latency.
+    for (;;) {
+        const hipError_t e = hipStreamQuery(f->stream);
+        if (e == hipSuccess) break;
+        if (e != hipErrorNotReady) return fail(PBF_ERR_HIP, std::string("hipStreamQuery: ") + hipGetErrorString(e));
+    }
     return PBF_OK;
 }
 
@@ -830,7 +903,7 @@ void* pbf_device_bitmap(pbf_filter_t* f) {
 int pbf_set_build_mode(pbf_filter_t* f, int mode) {
     if (!f) return fail(PBF_ERR_INVALID, "null filter handle");
     if (mode < PBF_BUILD_AUTO || mode > PBF_BUILD_TILED) return fail(PBF_ERR_INVALID, "bad build mode");
-    if (mode == PBF_BUILD_TILED && (!f->tiled_ok || f->k > 32))
+    if (mode == PBF_BUILD_TILED && (!f->tiled_ok || f->k > 32 || !part_fits(f->tm.nbuckets, f->k, false)))
         return fail(PBF_ERR_INVALID, "tiled build unsupported for this m / k");
     f->mode = mode;
     return PBF_OK;
@@ -841,7 +914,8 @@ int pbf_last_build_mode(pbf_filter_t* f) { return f ? f->last_mode : 0; }
 int pbf_set_probe_mode(pbf_filter_t* f, int mode) {
     if (!f) return fail(PBF_ERR_INVALID, "null filter handle");
     if (mode < PBF_PROBE_AUTO || mode > PBF_PROBE_TILED) return fail(PBF_ERR_INVALID, "bad probe mode");
-    if (mode == PBF_PROBE_TILED && (!f->tiled_ok || f->k > 32 || f->tm.tb > kSlotShift))
+    if (mode == PBF_PROBE_TILED &&
+        (!f->tiled_ok || f->k > 32 || f->tm.tb > kSlotShift || !part_fits(f->tm.nbuckets, f->k, true)))
         return fail(PBF_ERR_INVALID, "tiled probe unsupported for this m / k");
     f->probe_mode = mode;
     return PBF_OK;

@@ -1,0 +1,241 @@
+// Ring-buffer partition for the LDS-tiled build / probe (reference semantics:
+// src/bloom_filter.py:60-74), gfx950.  Used when the bitmap has many tiles (B >= ~128k
+// positions per sub-chunk key... see plan_ring in pebblebloom.hip), e.g. C2: m = 2^30, B = 1024.
+//
+// Why: the counting-sort partition (k_part) appends each sub-chunk's per-tile run (~18 entries,
+// ~72 B at C2) to its region with lane-parallel dword stores.  A run starts and ends inside
+// 64-B segments, and the fabric sees every piece as its own write request (measured: 7.0M write
+// requests, half of them 32-B partials, for 240 MB of entries); the write-out phase then runs at
+// the fabric's request rate.  Here every tile keeps a small FIFO ring in LDS; a sub-chunk appends
+// its positions to the rings (one LDS atomic + one LDS store per position, no scan, no stage),
+// and a flush phase writes every complete GS-entry group (64 B at GS = 16) with ONE wave store
+// instruction (4 lanes x 16 B), so each region line leaves as whole 64-B requests.
+//
+//   ring      RC entries per tile (RC = 2*GS).  head[b] = entries flushed (= the region write
+//             cursor, a multiple of GS), tail[b] = entries appended.  Entry e of tile b sits at
+//             ring[b*RC + (e % RC)] and lands at region position e.
+//   sub-chunk 1024 keys (one per thread).  The host picks the geometry so a tile receives ~GS/3
+//             positions per sub-chunk; a position that would overrun the ring (or the region
+//             capacity) leaves the stream like k_part's overflow (build: overflow list; probe:
+//             tested against the bitmap in place, a miss clears the key via `neg`).
+//   probe     entry = (j & 3) << 30 | slot << 20 | position-in-tile (slot = thread, j = sub-chunk).
+//             pref[g][q][b] = in-region entries of (g, b) before sub-chunk 4q, so k_gather_ring
+//             finds an entry's sub-chunk from its region position and the entry's j & 3.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "tiled_kernels.hpp"
+
+namespace pbf {
+
+constexpr uint32_t kRingKeysPerSub = 1024;  // = threads; slot field is 10 bits
+
+template <int KMAX, int KM, bool PROBE>
+__global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k, TileMap tm, PartGeom pg,
+                                                    uint32_t* __restrict__ regions, uint32_t* __restrict__ fill,
+                                                    uint32_t* __restrict__ pref, uint32_t* __restrict__ ovf,
+                                                    uint32_t* __restrict__ ovf_count,
+                                                    const uint32_t* __restrict__ bitmap, uint32_t* __restrict__ neg) {
+    extern __shared__ uint32_t smem[];
+    const uint32_t B = tm.nbuckets;
+    const uint32_t RC = pg.ring, GS = RC / 2, rmask = RC - 1;
+    const uint32_t tid = threadIdx.x, nt = blockDim.x;
+    const uint32_t lane = tid & 63, wave = tid >> 6;
+    const uint32_t g = blockIdx.x;
+    const uint32_t cap = pg.cap;
+    const uint32_t lmask = (1u << tm.tb) - 1u;
+    uint32_t* head = smem;                      // B
+    uint32_t* tail = head + B;                  // B
+    uint32_t* desc = tail + B;                  // 16 waves x 128 group descriptors
+    uint32_t* ring = smem + ((2 * B + 16 * 128 + 3) & ~3u);  // B * RC, 16-B aligned
+    const uint32_t nqs = pg.nq + 1;  // pref entries per (g, b)
+    for (uint32_t b = tid; b < B; b += nt) {
+        head[b] = tail[b] = 0;
+        if constexpr (PROBE) pref[(uint64_t(g) * B + b) * nqs] = 0;
+    }
+    const uint64_t k0 = uint64_t(g) * pg.kpw;
+    const uint64_t k1 = min(n, k0 + pg.kpw);
+    uint4 kw = make_uint4(0, 0, 0, 0);
+    if constexpr (KM == kFixed16) kw = reinterpret_cast<const uint4*>(ks.data)[min(k0 + tid, n - 1)];
+    uint32_t j = 0;
+    for (uint64_t s0 = k0; s0 < k1; s0 += kRingKeysPerSub, ++j) {
+        lds_barrier();  // previous flush done: head / tail stable, rings free
+        const uint64_t i = s0 + tid;
+        if (i < k1) {
+            uint32_t pos[KMAX > 0 ? KMAX : 1], slot[KMAX > 0 ? KMAX : 1];
+            auto emit = [&](int s, uint32_t h) {
+                const uint32_t p = tile_pos(h, tm);
+                pos[s] = p;
+                slot[s] = atomicAdd(tail + (p >> tm.tb), 1u);
+            };
+            if constexpr (KM == kFixed16) {
+                const uint4 w = kw;
+                if (s0 + kRingKeysPerSub < k1)  // next sub-chunk's key, in flight during this one
+                    kw = reinterpret_cast<const uint4*>(ks.data)[min(i + kRingKeysPerSub, n - 1)];
+                murmur_seeds16<KMAX>(w, k, emit);
+            } else {
+                hash_key<KMAX, KM>(ks, i, k, emit);
+            }
+#pragma unroll
+            for (int s = 0; s < KMAX; ++s) {
+                if (s < k) {
+                    const uint32_t p = pos[s], b = p >> tm.tb, e = slot[s];
+                    if (e - head[b] < RC && e < cap) {
+                        ring[b * RC + (e & rmask)] = PROBE ? (((j & 3u) << 30) | (tid << kSlotShift) | (p & lmask)) : p;
+                    } else if constexpr (PROBE) {  // ring or region full: test this position here
+                        const uint64_t bit = pos_to_bit(p, tm);
+                        if (!((bitmap[bit >> 5] >> (bit & 31)) & 1u)) atomicOr(neg + (i >> 5), 1u << (i & 31));
+                    } else {
+                        ovf[atomicAdd(ovf_count, 1u)] = p;
+                    }
+                }
+            }
+        }
+        lds_barrier();
+        // Flush: each wave owns 64 tiles per pass.  A lane's tile has 0..2 whole groups; the
+        // wave lists them (descriptor = tile | group << 16) and writes 64/(GS/4) groups per
+        // store instruction, GS/4 lanes x 16 B per group.
+        uint32_t* wd = desc + wave * 128;
+        const uint32_t lpg = GS / 4;          // lanes per group
+        const uint32_t gpi = 64 / lpg;        // groups per store instruction
+        for (uint32_t b0 = wave * 64; b0 < B; b0 += nt) {
+            const uint32_t b = b0 + lane;
+            uint32_t ng = 0, h = 0;
+            if (b < B) {
+                h = head[b];
+                const uint32_t t = min(tail[b], min(h + RC, cap));  // positions past these left the stream
+                tail[b] = t;
+                ng = (t - h) / GS;
+            }
+            const uint64_t m1 = __ballot(ng >= 1), m2 = __ballot(ng >= 2);
+            const uint64_t below = (uint64_t(1) << lane) - 1;
+            const uint32_t at = __popcll(m1 & below) + __popcll(m2 & below);
+            const uint32_t total = __popcll(m1) + __popcll(m2);
+            if (ng >= 1) wd[at] = b;
+            if (ng >= 2) wd[at + 1] = b | (1u << 16);
+            __builtin_amdgcn_wave_barrier();
+            for (uint32_t c0 = 0; c0 < total; c0 += gpi) {
+                const uint32_t gi = c0 + lane / lpg, q = lane % lpg;
+                if (gi < total) {
+                    const uint32_t d = wd[gi];
+                    const uint32_t tb = d & 0xFFFFu;
+                    const uint32_t e = head[tb] + (d >> 16) * GS + q * 4;  // region position
+                    const uint4 v = *reinterpret_cast<const uint4*>(ring + tb * RC + (e & rmask));
+                    *reinterpret_cast<uint4*>(regions + (uint64_t(g) * B + tb) * cap + e) = v;
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+            if (b < B) {
+                head[b] = h + ng * GS;
+                if constexpr (PROBE)
+                    if (((j + 1) & 3) == 0) pref[(uint64_t(g) * B + b) * nqs + ((j + 1) >> 2)] = tail[b];
+            }
+        }
+    }
+    lds_barrier();
+    // the last partial group of every tile, and the fill counts
+    for (uint32_t b = tid; b < B; b += nt) {
+        const uint32_t h = head[b], t = tail[b];
+        uint32_t* dst = regions + (uint64_t(g) * B + b) * cap;
+        for (uint32_t e = h; e < t; ++e) dst[e] = ring[b * RC + (e & rmask)];
+        fill[uint64_t(b) * pg.G + g] = t;
+        if constexpr (PROBE)
+            for (uint32_t q = (j + 3) >> 2; q <= pg.nq; ++q) pref[(uint64_t(g) * B + b) * nqs + q] = t;
+    }
+}
+
+// Probe gather for the ring partition: workgroup g owns keys [g*kpw, (g+1)*kpw) and regions
+// (g, 0..B-1).  Entries of sub-chunks 4q..4q+3 lie in [pref[q], pref[q+1]) of their region, so a
+// failed entry at position r belongs to sub-chunk 4q + (entry >> 30) with q the last group whose
+// pref[q] <= r; its key is that sub-chunk's first key + the entry's slot.  A failed entry clears
+// its key's bit in an LDS bitmap of the workgroup's keys, written out as hit-mask words.
+//   LDS: kbits[kpw/32], pref rows of the workgroup as u16 (B x (nq+1)).
+__global__ void __launch_bounds__(1024) k_gather_ring(TileMap tm, PartGeom pg, uint64_t n,
+                                                      const uint32_t* __restrict__ regions,
+                                                      const uint32_t* __restrict__ R, const uint32_t* __restrict__ fill,
+                                                      const uint32_t* __restrict__ pref,
+                                                      const uint32_t* __restrict__ neg, uint8_t* __restrict__ hitmask) {
+    extern __shared__ uint32_t smem[];
+    const uint32_t B = tm.nbuckets, cap = pg.cap, wpr = cap / 32, nqs = pg.nq + 1;
+    const uint32_t tid = threadIdx.x, nt = blockDim.x;
+    const uint32_t lane = tid & 63, wave = tid >> 6, nwaves = nt >> 6;
+    const uint32_t g = blockIdx.x;
+    const uint64_t k0 = uint64_t(g) * pg.kpw;
+    const uint64_t k1 = min(n, k0 + pg.kpw);
+    const uint32_t nkeys = uint32_t(k1 - k0);
+    const uint32_t kw = uint32_t((pg.kpw + 31) / 32);
+    uint32_t* kbits = smem;                                    // kw words
+    uint16_t* lpref = reinterpret_cast<uint16_t*>(kbits + kw);  // B * nqs (values <= cap < 2^16)
+    const uint32_t* gp = pref + uint64_t(g) * B * nqs;
+    for (uint32_t x = tid; x < B * nqs; x += nt) lpref[x] = uint16_t(gp[x]);
+    for (uint32_t w = tid; w < kw; w += nt) {
+        const uint32_t key0 = w * 32;
+        uint32_t m = key0 >= nkeys ? 0u : (nkeys - key0 >= 32 ? ~0u : ((1u << (nkeys - key0)) - 1u));
+        if (m) m &= ~neg[(k0 + key0) >> 5];  // k0 is a multiple of 64
+        kbits[w] = m;
+    }
+    lds_barrier();
+    constexpr int U = 4;
+    for (uint32_t b0 = wave; b0 < B; b0 += nwaves * U) {
+        uint32_t fillb[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) fillb[u] = b0 + u * nwaves < B ? fill[uint64_t(b0 + u * nwaves) * pg.G + g] : 0u;
+        uint32_t maxf = 0;
+#pragma unroll
+        for (int u = 0; u < U; ++u) maxf = max(maxf, fillb[u]);
+        for (uint32_t r0 = 0; r0 < maxf; r0 += 256) {
+            uint4 v[U];
+            uint32_t rw[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t b = min(b0 + u * nwaves, B - 1);
+                const uint32_t r = min(r0 + lane * 4, (max(fillb[u], 1u) - 1) & ~3u);
+                const uint64_t reg = uint64_t(g) * B + b;
+                v[u] = *reinterpret_cast<const uint4*>(regions + reg * cap + r);
+                rw[u] = R[reg * wpr + (r >> 5)];
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t b = b0 + u * nwaves;
+                const uint32_t r = r0 + lane * 4;
+                if (b < B && r < fillb[u]) {
+                    uint32_t fails = ~(rw[u] >> (r & 31)) & 0xFu;
+                    if (fillb[u] - r < 4) fails &= (1u << (fillb[u] - r)) - 1u;
+                    if (fails) {
+                        // q = the last group with pref[q] <= r (pref non-decreasing, pref[0] = 0)
+                        const uint16_t* pb = lpref + b * nqs;
+                        uint32_t lo = 0, len = nqs;
+                        while (len > 1) {
+                            const uint32_t half = len >> 1;
+                            if (pb[lo + half] <= r) lo += half;
+                            len -= half;
+                        }
+                        const uint32_t vv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+                        for (int t = 0; t < 4; ++t) {
+                            if ((fails >> t) & 1u) {
+                                while (lo + 1 < nqs && pb[lo + 1] <= r + t) ++lo;
+                                const uint32_t jj = lo * 4 + (vv[t] >> 30);
+                                const uint32_t key = jj * kRingKeysPerSub + ((vv[t] >> kSlotShift) & 1023u);
+                                atomicAnd(kbits + (key >> 5), ~(1u << (key & 31)));
+                            }
+                        }
+                    }
+                }
+            }
+        }
+    }
+    lds_barrier();
+    for (uint32_t w = tid; w * 32 < nkeys; w += nt) {
+        const uint64_t key0 = k0 + uint64_t(w) * 32;
+        const uint32_t bits = kbits[w];
+        const uint64_t nb = min<uint64_t>(4, (n - key0 + 7) / 8);
+        if (nb == 4 && (reinterpret_cast<uintptr_t>(hitmask + key0 / 8) & 3) == 0)
+            *reinterpret_cast<uint32_t*>(hitmask + key0 / 8) = bits;
+        else
+            for (uint64_t q = 0; q < nb; ++q) hitmask[key0 / 8 + q] = uint8_t(bits >> (8 * q));
+    }
+}
+
+}  // namespace pbf

@@ -50,6 +50,8 @@ struct PartGeom {
     uint32_t kps;      // keys per sub-chunk (kpt * 1024; <= 4096 for probes)
     uint32_t nsub;     // sub-chunks per workgroup
     uint64_t kpw;      // keys per workgroup (= nsub * kps)
+    uint32_t nq;       // ring partition: pref groups (4 sub-chunks each) per workgroup
+    uint32_t ring;     // ring partition: LDS ring entries per tile (0 = counting-sort partition)
 };
 
 constexpr uint32_t kSlotShift = 20;   // probe entry = slot-in-sub-chunk << 20 | position in tile
@@ -284,7 +286,11 @@ __global__ void __launch_bounds__(kPartThreads) k_part(KeySet ks, uint64_t n, in
         PBF_STAMP(6);
     }
     lds_barrier();
-    for (uint32_t b = tid; b < B; b += nt) fill[uint64_t(b) * pg.G + g] = min(cursor[b], pg.cap);
+    for (uint32_t b = tid; b < B; b += nt) {
+        fill[uint64_t(b) * pg.G + g] = min(cursor[b], pg.cap);
+        if constexpr (PROBE)  // the last workgroup may run fewer than nsub sub-chunks
+            for (uint32_t jj = j; jj < pg.nsub; ++jj) subcnt[(uint64_t(g) * pg.nsub + jj) * B + b] = 0;
+    }
 }
 
 // Copy nw words of the bitmap starting at word w0 into LDS (zero-filling up to W), with every
@@ -515,7 +521,8 @@ __global__ void __launch_bounds__(1024) k_gather(TileMap tm, PartGeom pg, uint64
         }
     }
     lds_barrier();
-    // one wave per region; U 64-entry windows (from different regions) in flight per wave
+    // one wave per region, 256 entries (one 16-byte load per lane) per step; U regions in
+    // flight per wave.  Regions start 128-B aligned (cap is a multiple of 32).
     constexpr int U = 4;
     for (uint32_t b0 = wave; b0 < B; b0 += nwaves * U) {
         uint32_t fillb[U];
@@ -524,31 +531,43 @@ __global__ void __launch_bounds__(1024) k_gather(TileMap tm, PartGeom pg, uint64
         uint32_t maxf = 0;
 #pragma unroll
         for (int u = 0; u < U; ++u) maxf = max(maxf, fillb[u]);
-        for (uint32_t r0 = 0; r0 < maxf; r0 += 64) {
-            uint32_t v[U], rw[U];
+        for (uint32_t r0 = 0; r0 < maxf; r0 += 256) {
+            uint4 v[U];
+            uint32_t rw[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const uint32_t b = min(b0 + u * nwaves, B - 1);
-                const uint32_t r = min(r0 + lane, max(fillb[u], 1u) - 1);
+                const uint32_t r = min(r0 + lane * 4, (max(fillb[u], 1u) - 1) & ~3u);
                 const uint64_t reg = uint64_t(g) * B + b;
-                v[u] = regions[reg * cap + r];
+                v[u] = *reinterpret_cast<const uint4*>(regions + reg * cap + r);
                 rw[u] = R[reg * wpr + (r >> 5)];
             }
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const uint32_t b = b0 + u * nwaves;
-                const uint32_t r = r0 + lane;
-                if (b < B && r < fillb[u] && !((rw[u] >> (r & 31)) & 1u)) {
-                    // sub-chunk of position r: the last j with pref[b][j] <= r
-                    const uint16_t* pb = pref + b * ps;
-                    uint32_t lo = 0, len = nsub;
-                    while (len > 1) {
-                        const uint32_t half = len >> 1;
-                        if (pb[lo + half] <= r) lo += half;
-                        len -= half;
+                const uint32_t r = r0 + lane * 4;
+                if (b < B && r < fillb[u]) {
+                    uint32_t fails = ~(rw[u] >> (r & 31)) & 0xFu;
+                    if (fillb[u] - r < 4) fails &= (1u << (fillb[u] - r)) - 1u;
+                    if (fails) {
+                        // sub-chunk of position r: the last j with pref[b][j] <= r
+                        const uint16_t* pb = pref + b * ps;
+                        uint32_t lo = 0, len = nsub;
+                        while (len > 1) {
+                            const uint32_t half = len >> 1;
+                            if (pb[lo + half] <= r) lo += half;
+                            len -= half;
+                        }
+                        const uint32_t vv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+                        for (int t = 0; t < 4; ++t) {
+                            if ((fails >> t) & 1u) {
+                                while (lo + 1 < nsub && pb[lo + 1] <= r + t) ++lo;
+                                const uint32_t key = lo * pg.kps + ((vv[t] >> kSlotShift) & kSlotMask);
+                                atomicAnd(kbits + (key >> 5), ~(1u << (key & 31)));
+                            }
+                        }
                     }
-                    const uint32_t key = lo * pg.kps + ((v[u] >> kSlotShift) & kSlotMask);
-                    atomicAnd(kbits + (key >> 5), ~(1u << (key & 31)));
                 }
             }
         }

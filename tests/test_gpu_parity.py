@@ -345,3 +345,47 @@ def test_sstable_section_roundtrip_golden():
     blob = encode_sstable(b"x" * 1000, b"m" * 77, big)
     again = decode_bloom_section(blob)
     assert again.bitmap() == big.bitmap() and again.nb_hash_functions == big.nb_hash_functions
+
+
+_PART_CHILD = """
+import numpy as np, sys
+sys.path.insert(0, '.')
+from pebbledb_amd import BloomFilter, PackedKeys
+from pebbledb_amd.keys import splitmix_hex_keys, varlen_keys
+from oracle.oracle import COracle
+o = COracle()
+# distinct keys, plus one key repeated 60k times: its tiles' regions / rings overflow
+distinct = splitmix_hex_keys(21, 0, 200000)
+same = np.repeat(splitmix_hex_keys(22, 0, 1), 60000, axis=0)
+fx = PackedKeys.fixed(np.concatenate([distinct, same, distinct[:1000]]))
+d, off = varlen_keys(23, 0, 100000)
+vr = PackedKeys(d, 100000, offsets=off)
+probes = PackedKeys.fixed(np.concatenate([splitmix_hex_keys(21, 150000, 100000), same,
+                                          np.repeat(splitmix_hex_keys(24, 0, 1), 50000, axis=0)]))
+# B = 1024 tiles (C2 geometry), 768 (non-power-of-two m), 16 (rings overflow constantly)
+for nb, pk, q in ((2 ** 27, fx, probes), (3 * 2 ** 25, vr, vr), (2 ** 21, fx, probes), (2 ** 27 + 12, vr, vr)):
+    want = o.build(nb, 6, pk, omp=True)
+    want_hm = o.probe(want, 6, q, omp=True)
+    bf = BloomFilter(nb, 6); bf.set_build_mode(2); bf.add_many(pk)
+    assert bf.bitmap() == want.tobytes(), nb
+    bf.add_many(pk)  # a second batch onto a non-pristine bitmap
+    assert bf.bitmap() == want.tobytes(), nb
+    bf.set_probe_mode(2)
+    assert np.array_equal(bf.may_contain_many(q, packed=True), want_hm), nb
+    assert bf.last_probe_mode == 2 and bf.last_build_mode == 2
+print('ok')
+"""
+
+
+@pytest.mark.parametrize("part", ["sort", "ring"])
+def test_tiled_partition_strategies_and_region_overflow(part):
+    """Both partition passes of the tiled build / probe (PBF_PART forces one), with a key
+    repeated enough to overflow its tiles' regions and rings (build overflow list, probe
+    in-place test)."""
+    import os
+    import subprocess
+    import sys
+    env = dict(os.environ, PBF_PART=part)
+    r = subprocess.run([sys.executable, "-c", _PART_CHILD], env=env, capture_output=True, text=True, timeout=600,
+                       cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]

@@ -13,7 +13,7 @@ run() {  # name seconds cmd...
   local rc=$?
   echo "== $name rc=$rc" | tee -a gpurun_out/session.log
   tail -n 30 "gpurun_out/$name.log"
-  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+  if [ $rc -ne 0 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
   return 0
 }
 for step in "$@"; do
@@ -32,7 +32,8 @@ for step in "$@"; do
          run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline
          run pmc_tcc 600 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum --output-format csv -d gpurun_out/pmc_tcc -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
     micro) run micro 300 tools/microbench/lds_rates ;;
-    phases) run phases 300 tools/microbench/part_phases ;;
+    phases) run phases_t0 300 tools/microbench/part_phases 0
+            run phases_t16 300 tools/microbench/part_phases 16 ;;
     gapdiag) run native0 120 tools/microbench/pipeline_bench 50 0
              run native1 120 tools/microbench/pipeline_bench 50 1
              run native2 120 tools/microbench/pipeline_bench 50 2
@@ -46,6 +47,15 @@ for step in "$@"; do
           run diag_c 300 python bench.py --steps 20 --warmup 5 --build-mode 2 --probe-mode 1 --no-cpu-baseline --sync-each-step
           run diag_d 300 python bench.py --steps 20 --warmup 5 --build-mode 2 --probe-mode 1 --no-cpu-baseline --no-events --sync-each-step
           run diag_e 300 python bench.py --steps 100 --warmup 5 --build-mode 2 --probe-mode 1 --no-cpu-baseline ;;
+    tdepth) for t in 0 8 16; do PBF_TDEPTH=$t run tdepth_$t 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-host-inclusive; done
+            for t in 0 8 16; do PBF_TDEPTH=$t run tdepth_prof_$t 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/tdprof_$t -o run -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-host-inclusive
+                              python tools/prof_summary.py gpurun_out/tdprof_$t > gpurun_out/tdprof_$t.txt 2>&1; done ;;
+    rep) run rep_long 300 python bench.py --steps 200 --warmup 5 --no-cpu-baseline --no-host-inclusive
+         for r in 1 2 3; do run rep_$r 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-host-inclusive; done
+         run rep_native 120 tools/microbench/pipeline_bench 50 0
+         run rep_native_ev 120 tools/microbench/pipeline_bench 50 1 ;;
+    wrreq) run counters 120 rocprofv3 -L
+           for t in 0 16; do PBF_TDEPTH=$t run wrreq_$t 300 rocprofv3 --pmc TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum --output-format csv -d gpurun_out/wrreq_$t -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-host-inclusive; done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

@@ -2,11 +2,13 @@
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -DPBF_STAMPS -o part_phases part_phases.hip
 // Shares (not absolute times) are what this build is good for: the stamps serialise.
 #include <cstdio>
+#include <cstdlib>
 #include <vector>
 #include "../../pebbledb_amd/csrc/tiled_kernels.hpp"
 using namespace pbf;
 
-int main() {
+int main(int argc, char** argv) {
+    const uint32_t T = argc > 1 ? uint32_t(atoi(argv[1])) : 0;
     const uint64_t n = 10000000, nb_bytes = 1ull << 27;
     const int k = 6;
     uint8_t* keys; hipMalloc(&keys, n * 16);
@@ -15,11 +17,11 @@ int main() {
     tm.im.m = nb_bytes * 8; tm.im.mode = kPow2; tm.im.mask = uint32_t(tm.im.m - 1);
     tm.tb = 20; tm.nbuckets = 1024; tm.total_words = nb_bytes / 4;
     for (int probe = 0; probe < 2; ++probe) {
-        const uint32_t B = 1024, kpt = 3, kps = kpt * 1024;
+        const uint32_t B = 1024, kpt = (probe && T > 8) ? 2 : 3, kps = kpt * 1024;
         PartGeom pg{};
         uint64_t kpw = (n + 255) / 256; kpw = (kpw + kps - 1) / kps * kps;
         pg.G = uint32_t((n + kpw - 1) / kpw); pg.kps = kps; pg.kpw = kpw; pg.nsub = uint32_t(kpw / kps);
-        pg.cap = 1024;
+        pg.cap = 1024; pg.tdepth = T;
         uint32_t *regions, *fill, *subcnt, *ovf, *cnt, *neg, *bitmap;
         hipMalloc(&regions, size_t(pg.G) * B * pg.cap * 4); hipMalloc(&fill, size_t(pg.G) * B * 4);
         hipMalloc(&subcnt, size_t(pg.G) * pg.nsub * B * 4); hipMalloc(&ovf, n * k * 4); hipMalloc(&cnt, 64);
@@ -28,7 +30,7 @@ int main() {
         unsigned long long* st; hipMalloc(&st, 64 * 8); hipMemset(st, 0, 64 * 8);
         hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &st, sizeof(st));
         KeySet ks{keys, nullptr, nullptr, 16};
-        const size_t lds = size_t(3 * B + 17) * 4 + size_t(kps) * k * (probe ? 6 : 4);
+        const size_t lds = size_t((3 * B + 17 + 3) & ~3u) * 4 + size_t(B) * T * 4 + size_t(kps) * k * (probe ? 6 : 4);
         hipEvent_t a, b; hipEventCreate(&a); hipEventCreate(&b);
         hipEventRecord(a);
         if (probe) {

@@ -14,7 +14,7 @@ passes=(
 )
 i=0
 for p in "${passes[@]}"; do
-  timeout -k 10 300 rocprofv3 --pmc $p --output-format csv -d "$out/p$i" -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline "$@" > "$out/p$i.log" 2>&1
+  timeout -k 10 300 rocprofv3 --pmc $p --output-format csv -d "$out/p$i" -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-host-inclusive "$@" > "$out/p$i.log" 2>&1
   rc=$?
   echo "pass $i rc=$rc"
   if [ $rc -ne 0 ]; then exit $rc; fi
