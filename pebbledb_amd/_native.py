@@ -9,7 +9,8 @@ import os
 import re
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libpebblebloom.so")
+# PBF_LIB: an alternative build of the same library (A/B measurements of kernel variants)
+LIB_PATH = os.environ.get("PBF_LIB") or os.path.join(_HERE, "libpebblebloom.so")
 HEADER = os.path.join(os.path.dirname(_HERE), "include", "pebblebloom.h")
 
 PBF_OK = 0

@@ -23,18 +23,23 @@ def up_to_date() -> bool:
     return all(os.path.getmtime(d) <= t for d in DEPS)
 
 
-def build_lib(force: bool = False, verbose: bool = True) -> str:
-    if not force and up_to_date():
+def build_lib(force: bool = False, verbose: bool = True, out: str = LIB, defines=()) -> str:
+    """Compile libpebblebloom.so (or, for A/B measurements, a variant with extra -D defines
+    into `out`; select it at run time with PBF_LIB)."""
+    if not force and out == LIB and not defines and up_to_date():
         return LIB
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-Wall", "-Wno-unused-result", "-o", LIB + ".tmp"] + SOURCES
+           "-Wall", "-Wno-unused-result"] + [f"-D{d}" for d in defines] + ["-o", out + ".tmp"] + SOURCES
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
-    os.replace(LIB + ".tmp", LIB)
-    return LIB
+    os.replace(out + ".tmp", out)
+    return out
 
 
 if __name__ == "__main__":
-    build_lib(force="--force" in sys.argv)
-    print(LIB)
+    # python -m pebbledb_amd.build [--force] [--out PATH -DNAME ...]
+    args = sys.argv[1:]
+    out = args[args.index("--out") + 1] if "--out" in args else LIB
+    defs = [a[2:] for a in args if a.startswith("-D")]
+    print(build_lib(force="--force" in args or out != LIB, out=out, defines=defs))

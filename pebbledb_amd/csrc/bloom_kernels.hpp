@@ -32,15 +32,15 @@ struct KeySet {
     uint32_t key_len;         // kFixed*
 };
 
-// Hash key i with seeds 0..k-1 and call emit(seed, hash_u32).
+// Hash key i with seeds sbase..sbase+k-1 and call emit(s, hash_u32), s = 0..k-1.
 template <int KMAX, int KM, class Emit>
-__device__ __forceinline__ void hash_key(const KeySet& ks, uint64_t i, int k, Emit&& emit) {
+__device__ __forceinline__ void hash_key(const KeySet& ks, uint64_t i, int k, Emit&& emit, int sbase = 0) {
     if constexpr (KM == kFixed16) {
         const uint4 w = reinterpret_cast<const uint4*>(ks.data)[i];
         if constexpr (KMAX == 0) {
-            murmur_seeds_loop(ks.data + i * 16, 16u, k, emit);
+            murmur_seeds_loop(ks.data + i * 16, 16u, k, emit, sbase);
         } else {
-            murmur_seeds16<KMAX>(w, k, emit);
+            murmur_seeds16<KMAX>(w, k, emit, sbase);
         }
     } else {
         const uint8_t* p;
@@ -56,9 +56,9 @@ __device__ __forceinline__ void hash_key(const KeySet& ks, uint64_t i, int k, Em
             len = uint32_t(b - a);
         }
         if constexpr (KMAX == 0) {
-            murmur_seeds_loop(p, len, k, emit);
+            murmur_seeds_loop(p, len, k, emit, sbase);
         } else {
-            murmur_seeds<KMAX>(p, len, k, emit);
+            murmur_seeds<KMAX>(p, len, k, emit, sbase);
         }
     }
 }

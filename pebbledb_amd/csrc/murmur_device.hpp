@@ -60,13 +60,14 @@ __device__ __forceinline__ uint32_t load_tail(const uint8_t* p, uint32_t t) {
     return v & ((1u << (8 * t)) - 1u);
 }
 
-// All k seeds of MurmurHash3_x86_32 for one key; emit(seed, hash_u32) is called for
-// seed = 0..k-1.  KMAX is the compile-time register budget for seed states (k <= KMAX).
+// k seeds of MurmurHash3_x86_32 for one key, sbase .. sbase+k-1; emit(s, hash_u32) is called
+// for s = 0..k-1 (seed sbase + s).  KMAX is the compile-time register budget for seed states
+// (k <= KMAX).
 template <int KMAX, class Emit>
-__device__ __forceinline__ void murmur_seeds(const uint8_t* p, uint32_t len, int k, Emit&& emit) {
+__device__ __forceinline__ void murmur_seeds(const uint8_t* p, uint32_t len, int k, Emit&& emit, int sbase = 0) {
     uint32_t h[KMAX];
 #pragma unroll
-    for (int s = 0; s < KMAX; ++s) h[s] = uint32_t(s);
+    for (int s = 0; s < KMAX; ++s) h[s] = uint32_t(sbase + s);
     const uint32_t nb = len >> 2;
     const bool aligned = (reinterpret_cast<uintptr_t>(p) & 3) == 0;
     if (aligned) {
@@ -96,12 +97,12 @@ __device__ __forceinline__ void murmur_seeds(const uint8_t* p, uint32_t len, int
 
 // Fixed 16-byte keys from one 16-byte load (the C2/C4/C5 key shape).
 template <int KMAX, class Emit>
-__device__ __forceinline__ void murmur_seeds16(uint4 w, int k, Emit&& emit) {
+__device__ __forceinline__ void murmur_seeds16(uint4 w, int k, Emit&& emit, int sbase = 0) {
     const uint32_t m0 = mix_block(w.x), m1 = mix_block(w.y), m2 = mix_block(w.z), m3 = mix_block(w.w);
 #pragma unroll
     for (int s = 0; s < KMAX; ++s) {
         if (s < k) {
-            uint32_t h = uint32_t(s);
+            uint32_t h = uint32_t(sbase + s);
             h = round_h(h, m0);
             h = round_h(h, m1);
             h = round_h(h, m2);
@@ -113,11 +114,11 @@ __device__ __forceinline__ void murmur_seeds16(uint4 w, int k, Emit&& emit) {
 
 // Runtime-k fallback (k > 32): one seed at a time, key bytes re-read (from L1) per seed.
 template <class Emit>
-__device__ __forceinline__ void murmur_seeds_loop(const uint8_t* p, uint32_t len, int k, Emit&& emit) {
+__device__ __forceinline__ void murmur_seeds_loop(const uint8_t* p, uint32_t len, int k, Emit&& emit, int sbase = 0) {
     const uint32_t nb = len >> 2;
     const uint32_t t = len & 3;
     for (int s = 0; s < k; ++s) {
-        uint32_t h = uint32_t(s);
+        uint32_t h = uint32_t(sbase + s);
         for (uint32_t b = 0; b < nb; ++b) h = round_h(h, mix_block(load_u32_any(p + 4 * b)));
         if (t) h ^= mix_block(load_tail(p + 4 * nb, t));
         emit(s, fmix32(h ^ len));

@@ -97,6 +97,17 @@ size_t stage_bytes() {
 }
 constexpr uint64_t kMaxPositions = uint64_t(1) << 30; // tiled pipeline batch (4 GiB of positions)
 
+// Rounds of the ring-partition tiled probe (PBF_PROBE_ROUNDS=2 selects two; default one: the
+// second round still pays the partition's per-sub-chunk cost for every key, measured slower).
+int probe_rounds() {
+    static const int v = [] {
+        const char* e = std::getenv("PBF_PROBE_ROUNDS");
+        const int x = e ? std::atoi(e) : 0;
+        return x > 0 ? x : 1;
+    }();
+    return v;
+}
+
 // Words loaded in the probe's first stage (PBF_PROBE_S1 overrides; tuning knob).
 int probe_stage1() {
     static const int v = [] {
@@ -194,7 +205,7 @@ struct pbf_filter {
     bool tiled_ok = false;
     int probe_mode = PBF_PROBE_AUTO;
     int last_probe_mode = 0;
-    DevBuf regions, fill, ovf, ovf_count, subcnt, rbits, neg;
+    DevBuf regions, fill, ovf, ovf_count, subcnt, rbits, neg, alive;
     DevBuf dkeys, doffs, dout;
     PinBuf pin[2];
     int pin_next = 0;
@@ -279,8 +290,10 @@ int part_override() {
 // only a few positions into each tile (<= GS/2 on average), which is what the ring's GS-entry
 // groups need, while the counting-sort partition's per-tile runs get too short to write well.
 // Ring of 32 entries (64-B groups) up to 1024 tiles, of 16 (32-B groups) up to 2048.
+bool ring_pow2(const TileMap& tm) { return tm.im.mode == kPow2 && !tm.cspace; }
+
 uint32_t ring_entries(uint32_t B, uint32_t k, bool probe, uint32_t tb) {
-    if (probe && tb > kSlotShift) return 0;
+    if ((probe && tb > kSlotShift) || k > 16) return 0;
     const int ov = part_override();
     if (ov == 1) return 0;
     const uint32_t rc = B <= 1024 ? 32 : (B <= 2048 ? 16 : 0);
@@ -336,7 +349,11 @@ PartPlan plan_partition(uint32_t B, uint32_t k, int km, uint64_t n, bool probe) 
 
 PartPlan plan_for(uint32_t B, uint32_t k, int km, uint64_t n, bool probe, uint32_t tb) {
     const uint32_t rc = ring_entries(B, k, probe, tb);
-    return rc ? plan_ring(B, k, n, rc) : plan_partition(B, k, km, n, probe);
+    if (rc) {
+        const PartPlan pl = plan_ring(B, k, n, rc);
+        if (pl.pg.cap < (1u << 20)) return pl;  // flush descriptors hold a region position in 20 bits
+    }
+    return plan_partition(B, k, km, n, probe);
 }
 
 int run_tiled(pbf_filter_t* f, const Batch& b) {
@@ -358,12 +375,22 @@ int run_tiled(pbf_filter_t* f, const Batch& b) {
     hipError_t err = hipSuccess;
     dispatch(kmax_for(k), b.km, [&](auto KMAX, auto KM) {
         if constexpr (decltype(KMAX)::value > 0) {  // tiled path only for k <= 32
-            auto kern = pg.ring ? k_part_ring<decltype(KMAX)::value, decltype(KM)::value, false>
-                                : k_part<decltype(KMAX)::value, decltype(KM)::value, false>;
-            err = allow_lds(kern, pl.lds_part);
-            if (err == hipSuccess)
-                kern<<<pg.G, kPartThreads, pl.lds_part, s>>>(b.ks, b.n, int(k), tm, pg, regions, fill, nullptr, ovf,
-                                                     ovf_count, nullptr, nullptr);
+            constexpr int KX = decltype(KMAX)::value, KMD = decltype(KM)::value;
+            if (pg.ring) {
+                if constexpr (KX <= 16) {
+                    auto kern = ring_pow2(tm) ? k_part_ring<KX, KMD, false, true> : k_part_ring<KX, KMD, false, false>;
+                    err = allow_lds(kern, pl.lds_part);
+                    if (err == hipSuccess)
+                        kern<<<pg.G, kPartThreads, pl.lds_part, s>>>(b.ks, b.n, int(k), tm, pg, regions, fill, nullptr,
+                                                             ovf, ovf_count, nullptr, nullptr, 0, nullptr);
+                }
+            } else {
+                auto kern = k_part<KX, KMD, false>;
+                err = allow_lds(kern, pl.lds_part);
+                if (err == hipSuccess)
+                    kern<<<pg.G, kPartThreads, pl.lds_part, s>>>(b.ks, b.n, int(k), tm, pg, regions, fill, nullptr, ovf,
+                                                         ovf_count, nullptr, nullptr);
+            }
         }
     });
     HIP_TRY(err);
@@ -397,36 +424,57 @@ int run_tiled_probe(pbf_filter_t* f, const Batch& b, uint8_t* hitmask) {
     auto* R = static_cast<uint32_t*>(f->rbits.p);
     auto* neg = static_cast<uint32_t*>(f->neg.p);
     hipStream_t s = f->stream;
-    HIP_TRY(hipMemsetAsync(neg, 0, neg_bytes, s));
-    hipError_t err = hipSuccess;
-    dispatch(kmax_for(k), b.km, [&](auto KMAX, auto KM) {
-        if constexpr (decltype(KMAX)::value > 0) {
-            auto kern = pg.ring ? k_part_ring<decltype(KMAX)::value, decltype(KM)::value, true>
-                                : k_part<decltype(KMAX)::value, decltype(KM)::value, true>;
-            err = allow_lds(kern, pl.lds_part);
-            if (err == hipSuccess)
-                kern<<<pg.G, kPartThreads, pl.lds_part, s>>>(b.ks, b.n, int(k), tm, pg, regions, fill, subcnt, nullptr,
-                                                     nullptr, f->bitmap, neg);
-        }
-    });
-    HIP_TRY(err);
-    CHECK_LAUNCH();
     size_t lds_tile = ((size_t(1) << tm.tb) / 32 + 2 * pg.G + 1 + 16) * 4;
     const size_t lds_expand = size_t(pg.G) * (pg.cap / 32) * 2;
     const int expand = lds_tile + lds_expand <= 160 * 1024 ? 1 : 0;
     if (expand) lds_tile += lds_expand;
     HIP_TRY(allow_lds(k_tile_probe, lds_tile));
-    k_tile_probe<<<B, 1024, lds_tile, s>>>(tm, pg, regions, fill, f->bitmap, R, expand);
-    CHECK_LAUNCH();
-    if (pg.ring) {
-        HIP_TRY(allow_lds(k_gather_ring, pl.lds_gather));
-        k_gather_ring<<<pg.G, 1024, pl.lds_gather, s>>>(tm, pg, b.n, regions, R, fill, subcnt, neg, hitmask);
-    } else {
-        HIP_TRY(allow_lds(k_gather, pl.lds_gather));
-        k_gather<<<pg.G, 1024, pl.lds_gather, s>>>(tm, pg, b.n, regions, R, subcnt, neg, hitmask);
-    }
-    CHECK_LAUNCH();
-    return PBF_OK;
+    // One probe round: seeds [sbase, sbase + kr) of the keys `alive` marks (all if null), the
+    // round's hit mask (AND alive) into `out`.
+    auto round = [&](int sbase, uint32_t kr, const uint32_t* alive, uint8_t* out) -> int {
+        HIP_TRY(hipMemsetAsync(neg, 0, neg_bytes, s));
+        hipError_t err = hipSuccess;
+        dispatch(kmax_for(kr), b.km, [&](auto KMAX, auto KM) {
+            if constexpr (decltype(KMAX)::value > 0) {
+                constexpr int KX = decltype(KMAX)::value, KMD = decltype(KM)::value;
+                if (pg.ring) {
+                    if constexpr (KX <= 16) {
+                        auto kern = ring_pow2(tm) ? k_part_ring<KX, KMD, true, true> : k_part_ring<KX, KMD, true, false>;
+                        err = allow_lds(kern, pl.lds_part);
+                        if (err == hipSuccess)
+                            kern<<<pg.G, kPartThreads, pl.lds_part, s>>>(b.ks, b.n, int(kr), tm, pg, regions, fill,
+                                                                 subcnt, nullptr, nullptr, f->bitmap, neg, sbase, alive);
+                    }
+                } else {
+                    auto kern = k_part<KX, KMD, true>;
+                    err = allow_lds(kern, pl.lds_part);
+                    if (err == hipSuccess)
+                        kern<<<pg.G, kPartThreads, pl.lds_part, s>>>(b.ks, b.n, int(kr), tm, pg, regions, fill, subcnt,
+                                                             nullptr, nullptr, f->bitmap, neg);
+                }
+            }
+        });
+        HIP_TRY(err);
+        CHECK_LAUNCH();
+        k_tile_probe<<<B, 1024, lds_tile, s>>>(tm, pg, regions, fill, f->bitmap, R, expand);
+        CHECK_LAUNCH();
+        if (pg.ring) {
+            HIP_TRY(allow_lds(k_gather_ring, pl.lds_gather));
+            k_gather_ring<<<pg.G, 1024, pl.lds_gather, s>>>(tm, pg, b.n, regions, R, fill, subcnt, neg, alive, out);
+        } else {
+            HIP_TRY(allow_lds(k_gather, pl.lds_gather));
+            k_gather<<<pg.G, 1024, pl.lds_gather, s>>>(tm, pg, b.n, regions, R, subcnt, neg, out);
+        }
+        CHECK_LAUNCH();
+        return PBF_OK;
+    };
+    if (!pg.ring || k < 2 || probe_rounds() < 2) return round(0, k, nullptr, hitmask);
+    // two rounds: seed 0 for every key, then seeds 1..k-1 for the keys seed 0 left alive
+    HIP_TRY(f->alive.ensure(neg_bytes));
+    auto* alive = static_cast<uint32_t*>(f->alive.p);
+    int rc = round(0, 1, nullptr, reinterpret_cast<uint8_t*>(alive));
+    if (rc) return rc;
+    return round(1, k - 1, alive, hitmask);
 }
 
 // The partition pass needs its tile counters plus a stage of one key per thread in LDS.
@@ -759,7 +807,8 @@ int pbf_destroy(pbf_filter_t* f) {
     if (f->stream) (void)hipStreamSynchronize(f->stream);
     if (f->bitmap) (void)hipFree(f->bitmap);
     if (f->dpop) (void)hipFree(f->dpop);
-    for (DevBuf* d : {&f->regions, &f->fill, &f->ovf, &f->ovf_count, &f->subcnt, &f->rbits, &f->neg}) d->release();
+    for (DevBuf* d : {&f->regions, &f->fill, &f->ovf, &f->ovf_count, &f->subcnt, &f->rbits, &f->neg, &f->alive})
+        d->release();
     f->dkeys.release();
     f->doffs.release();
     f->dout.release();

@@ -21,6 +21,10 @@
 //   probe     entry = (j & 3) << 30 | slot << 20 | position-in-tile (slot = thread, j = sub-chunk).
 //             pref[g][q][b] = in-region entries of (g, b) before sub-chunk 4q, so k_gather_ring
 //             finds an entry's sub-chunk from its region position and the entry's j & 3.
+//   rounds    The probe runs in two rounds, the batched form of may_contain's early exit
+//             (bloom_filter.py:71-73): round 1 tests seed 0 of every key; round 2 tests seeds
+//             1..k-1 of the keys round 1 left alive (`alive`, the round-1 hit mask), so a
+//             non-member usually costs one position instead of k.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -30,14 +34,29 @@
 namespace pbf {
 
 constexpr uint32_t kRingKeysPerSub = 1024;  // = threads; slot field is 10 bits
+#ifndef PBF_RING_PREFETCH
+#define PBF_RING_PREFETCH 4
+#endif
+constexpr int kRingPrefetch = PBF_RING_PREFETCH;  // sub-chunks of keys loaded per batch
 
-template <int KMAX, int KM, bool PROBE>
+// Tile position of a hash when m is a power of two <= 2^32 (POW2) or in general.
+template <bool POW2>
+__device__ __forceinline__ uint32_t ring_pos(uint32_t h, const TileMap& tm) {
+    if constexpr (POW2) return h & tm.im.mask;
+    return tile_pos(h, tm);
+}
+
+// Keys are loaded kRingPrefetch sub-chunks at a time, one batch ahead.  On gfx950 vmcnt also
+// counts stores, so the wait for a key load also waits for every flush store issued before it;
+// batching pays that wait once per kRingPrefetch sub-chunks instead of once per sub-chunk.
+template <int KMAX, int KM, bool PROBE, bool POW2>
 __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k, TileMap tm, PartGeom pg,
                                                     uint32_t* __restrict__ regions, uint32_t* __restrict__ fill,
                                                     uint32_t* __restrict__ pref, uint32_t* __restrict__ ovf,
                                                     uint32_t* __restrict__ ovf_count,
-                                                    const uint32_t* __restrict__ bitmap, uint32_t* __restrict__ neg) {
-    extern __shared__ uint32_t smem[];
+                                                    const uint32_t* __restrict__ bitmap, uint32_t* __restrict__ neg,
+                                                    int sbase, const uint32_t* __restrict__ alive) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     const uint32_t B = tm.nbuckets;
     const uint32_t RC = pg.ring, GS = RC / 2, rmask = RC - 1;
     const uint32_t tid = threadIdx.x, nt = blockDim.x;
@@ -45,9 +64,9 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
     const uint32_t g = blockIdx.x;
     const uint32_t cap = pg.cap;
     const uint32_t lmask = (1u << tm.tb) - 1u;
-    uint32_t* head = smem;                      // B
-    uint32_t* tail = head + B;                  // B
-    uint32_t* desc = tail + B;                  // 16 waves x 128 group descriptors
+    uint32_t* head = smem;                                   // B
+    uint32_t* tail = head + B;                               // B
+    uint32_t* desc = tail + B;                               // 16 waves x 128 group descriptors
     uint32_t* ring = smem + ((2 * B + 16 * 128 + 3) & ~3u);  // B * RC, 16-B aligned
     const uint32_t nqs = pg.nq + 1;  // pref entries per (g, b)
     for (uint32_t b = tid; b < B; b += nt) {
@@ -56,81 +75,133 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
     }
     const uint64_t k0 = uint64_t(g) * pg.kpw;
     const uint64_t k1 = min(n, k0 + pg.kpw);
-    uint4 kw = make_uint4(0, 0, 0, 0);
-    if constexpr (KM == kFixed16) kw = reinterpret_cast<const uint4*>(ks.data)[min(k0 + tid, n - 1)];
-    uint32_t j = 0;
-    for (uint64_t s0 = k0; s0 < k1; s0 += kRingKeysPerSub, ++j) {
-        lds_barrier();  // previous flush done: head / tail stable, rings free
-        const uint64_t i = s0 + tid;
-        if (i < k1) {
-            uint32_t pos[KMAX > 0 ? KMAX : 1], slot[KMAX > 0 ? KMAX : 1];
-            auto emit = [&](int s, uint32_t h) {
-                const uint32_t p = tile_pos(h, tm);
-                pos[s] = p;
-                slot[s] = atomicAdd(tail + (p >> tm.tb), 1u);
-            };
-            if constexpr (KM == kFixed16) {
-                const uint4 w = kw;
-                if (s0 + kRingKeysPerSub < k1)  // next sub-chunk's key, in flight during this one
-                    kw = reinterpret_cast<const uint4*>(ks.data)[min(i + kRingKeysPerSub, n - 1)];
-                murmur_seeds16<KMAX>(w, k, emit);
-            } else {
-                hash_key<KMAX, KM>(ks, i, k, emit);
-            }
+    constexpr int P = kRingPrefetch;
+    constexpr bool F16 = KM == kFixed16;
+    uint4 kw[F16 ? P : 1];
+    uint32_t aw[P];  // alive words of this thread's keys (probe round 2)
+    auto load_batch = [&](uint64_t c0) {
 #pragma unroll
-            for (int s = 0; s < KMAX; ++s) {
-                if (s < k) {
-                    const uint32_t p = pos[s], b = p >> tm.tb, e = slot[s];
-                    if (e - head[b] < RC && e < cap) {
-                        ring[b * RC + (e & rmask)] = PROBE ? (((j & 3u) << 30) | (tid << kSlotShift) | (p & lmask)) : p;
-                    } else if constexpr (PROBE) {  // ring or region full: test this position here
-                        const uint64_t bit = pos_to_bit(p, tm);
-                        if (!((bitmap[bit >> 5] >> (bit & 31)) & 1u)) atomicOr(neg + (i >> 5), 1u << (i & 31));
-                    } else {
-                        ovf[atomicAdd(ovf_count, 1u)] = p;
+        for (int u = 0; u < P; ++u) {
+            const uint64_t i = c0 + uint64_t(u) * kRingKeysPerSub + tid;
+            aw[u] = (alive && i < k1) ? alive[i >> 5] : ~0u;
+            if constexpr (F16) kw[u] = reinterpret_cast<const uint4*>(ks.data)[min(i, n - 1)];
+        }
+    };
+    load_batch(k0);
+    uint32_t j = 0;
+    for (uint64_t c0 = k0; c0 < k1; c0 += uint64_t(P) * kRingKeysPerSub) {
+        uint4 cw[F16 ? P : 1];
+        uint32_t ca[P];
+#pragma unroll
+        for (int u = 0; u < P; ++u) {
+            if constexpr (F16) cw[u] = kw[u];
+            ca[u] = aw[u];
+        }
+        if (c0 + uint64_t(P) * kRingKeysPerSub < k1) load_batch(c0 + uint64_t(P) * kRingKeysPerSub);
+#pragma unroll
+        for (int u = 0; u < P; ++u, ++j) {
+            const uint64_t s0 = c0 + uint64_t(u) * kRingKeysPerSub;
+            if (s0 >= k1) break;
+            const uint64_t i = s0 + tid;
+            // a probe round after the first hashes only keys that are still possible members
+            const bool live = i < k1 && ((ca[u] >> (i & 31)) & 1u);
+            uint32_t pos[KMAX], slot[KMAX], hd[KMAX];
+            auto hash = [&] {
+                auto emit = [&](int s, uint32_t h) { pos[s] = ring_pos<POW2>(h, tm); };
+                if constexpr (F16)
+                    murmur_seeds16<KMAX>(cw[u], k, emit, sbase);
+                else
+                    hash_key<KMAX, KM>(ks, i, k, emit, sbase);
+            };
+#ifndef PBF_RING_HASH_LATE
+            // hash before the barrier: a wave done with its share of the previous flush hashes
+            // while the others still flush
+            if (live) hash();
+#endif
+            PBF_STAMP(0);
+            lds_barrier();  // previous flush done: head / tail stable, rings free
+            PBF_STAMP(1);
+#ifdef PBF_RING_HASH_LATE
+            if (live) hash();
+#endif
+            if (live) {
+#pragma unroll
+                for (int s = 0; s < KMAX; ++s) {
+                    if (s < k) {
+                        slot[s] = atomicAdd(tail + (pos[s] >> tm.tb), 1u);
+                        hd[s] = head[pos[s] >> tm.tb];
+                    }
+                }
+                PBF_STAMP(2);
+                uint32_t spill = 0;  // positions that overrun their tile's ring or region
+#pragma unroll
+                for (int s = 0; s < KMAX; ++s) {
+                    if (s < k) {
+                        const uint32_t p = pos[s], b = p >> tm.tb, e = slot[s];
+                        if (e - hd[s] < RC && e < cap)
+                            ring[b * RC + (e & rmask)] =
+                                PROBE ? (((j & 3u) << 30) | (tid << kSlotShift) | (p & lmask)) : p;
+                        else
+                            spill |= 1u << s;
+                    }
+                }
+                if (spill) {  // rare (heavy key duplication): out of the stream
+#pragma unroll
+                    for (int s = 0; s < KMAX; ++s) {
+                        if ((spill >> s) & 1u) {
+                            if constexpr (PROBE) {  // test this position here
+                                const uint64_t bit = pos_to_bit(pos[s], tm);
+                                if (!((bitmap[bit >> 5] >> (bit & 31)) & 1u)) atomicOr(neg + (i >> 5), 1u << (i & 31));
+                            } else {
+                                ovf[atomicAdd(ovf_count, 1u)] = pos[s];
+                            }
+                        }
                     }
                 }
             }
-        }
-        lds_barrier();
-        // Flush: each wave owns 64 tiles per pass.  A lane's tile has 0..2 whole groups; the
-        // wave lists them (descriptor = tile | group << 16) and writes 64/(GS/4) groups per
-        // store instruction, GS/4 lanes x 16 B per group.
-        uint32_t* wd = desc + wave * 128;
-        const uint32_t lpg = GS / 4;          // lanes per group
-        const uint32_t gpi = 64 / lpg;        // groups per store instruction
-        for (uint32_t b0 = wave * 64; b0 < B; b0 += nt) {
-            const uint32_t b = b0 + lane;
-            uint32_t ng = 0, h = 0;
-            if (b < B) {
-                h = head[b];
-                const uint32_t t = min(tail[b], min(h + RC, cap));  // positions past these left the stream
-                tail[b] = t;
-                ng = (t - h) / GS;
-            }
-            const uint64_t m1 = __ballot(ng >= 1), m2 = __ballot(ng >= 2);
-            const uint64_t below = (uint64_t(1) << lane) - 1;
-            const uint32_t at = __popcll(m1 & below) + __popcll(m2 & below);
-            const uint32_t total = __popcll(m1) + __popcll(m2);
-            if (ng >= 1) wd[at] = b;
-            if (ng >= 2) wd[at + 1] = b | (1u << 16);
-            __builtin_amdgcn_wave_barrier();
-            for (uint32_t c0 = 0; c0 < total; c0 += gpi) {
-                const uint32_t gi = c0 + lane / lpg, q = lane % lpg;
-                if (gi < total) {
-                    const uint32_t d = wd[gi];
-                    const uint32_t tb = d & 0xFFFFu;
-                    const uint32_t e = head[tb] + (d >> 16) * GS + q * 4;  // region position
-                    const uint4 v = *reinterpret_cast<const uint4*>(ring + tb * RC + (e & rmask));
-                    *reinterpret_cast<uint4*>(regions + (uint64_t(g) * B + tb) * cap + e) = v;
+            PBF_STAMP(3);
+            lds_barrier();
+            PBF_STAMP(4);
+            // Flush: each wave owns 64 tiles per pass.  A lane's tile has 0..2 whole groups;
+            // the wave lists them (descriptor = tile | region position << 12) and writes
+            // 64/(GS/4) groups per store instruction, GS/4 lanes x 16 B per group, each whole.
+            uint32_t* wd = desc + wave * 128;
+            const uint32_t lpg = GS / 4;    // lanes per group
+            const uint32_t gpi = 64 / lpg;  // groups per store instruction
+            for (uint32_t b0 = wave * 64; b0 < B; b0 += nt) {
+                const uint32_t b = b0 + lane;
+                uint32_t ng = 0, h = 0;
+                if (b < B) {
+                    h = head[b];
+                    const uint32_t t = min(tail[b], min(h + RC, cap));  // positions past these left the stream
+                    tail[b] = t;
+                    ng = (t - h) / GS;
+                }
+                const uint64_t m1 = __ballot(ng >= 1), m2 = __ballot(ng >= 2);
+                const uint64_t below = (uint64_t(1) << lane) - 1;
+                const uint32_t at = __popcll(m1 & below) + __popcll(m2 & below);
+                const uint32_t total = __popcll(m1) + __popcll(m2);
+                if (ng >= 1) wd[at] = b | (h << 12);
+                if (ng >= 2) wd[at + 1] = b | ((h + GS) << 12);
+                __builtin_amdgcn_wave_barrier();
+                for (uint32_t c = 0; c < total; c += gpi) {
+                    const uint32_t gi = c + lane / lpg, q = lane % lpg;
+                    if (gi < total) {
+                        const uint32_t d = wd[gi];
+                        const uint32_t tb = d & 0xFFFu;
+                        const uint32_t e = (d >> 12) + q * 4;  // region position
+                        const uint4 v = *reinterpret_cast<const uint4*>(ring + tb * RC + (e & rmask));
+                        *reinterpret_cast<uint4*>(regions + (uint64_t(g) * B + tb) * cap + e) = v;
+                    }
+                }
+                __builtin_amdgcn_wave_barrier();
+                if (b < B) {
+                    head[b] = h + ng * GS;
+                    if constexpr (PROBE)
+                        if (((j + 1) & 3) == 0) pref[(uint64_t(g) * B + b) * nqs + ((j + 1) >> 2)] = tail[b];
                 }
             }
-            __builtin_amdgcn_wave_barrier();
-            if (b < B) {
-                head[b] = h + ng * GS;
-                if constexpr (PROBE)
-                    if (((j + 1) & 3) == 0) pref[(uint64_t(g) * B + b) * nqs + ((j + 1) >> 2)] = tail[b];
-            }
+            PBF_STAMP(5);
         }
     }
     lds_barrier();
@@ -155,7 +226,8 @@ __global__ void __launch_bounds__(1024) k_gather_ring(TileMap tm, PartGeom pg, u
                                                       const uint32_t* __restrict__ regions,
                                                       const uint32_t* __restrict__ R, const uint32_t* __restrict__ fill,
                                                       const uint32_t* __restrict__ pref,
-                                                      const uint32_t* __restrict__ neg, uint8_t* __restrict__ hitmask) {
+                                                      const uint32_t* __restrict__ neg, const uint32_t* __restrict__ alive,
+                                                      uint8_t* __restrict__ hitmask) {
     extern __shared__ uint32_t smem[];
     const uint32_t B = tm.nbuckets, cap = pg.cap, wpr = cap / 32, nqs = pg.nq + 1;
     const uint32_t tid = threadIdx.x, nt = blockDim.x;
@@ -172,7 +244,10 @@ __global__ void __launch_bounds__(1024) k_gather_ring(TileMap tm, PartGeom pg, u
     for (uint32_t w = tid; w < kw; w += nt) {
         const uint32_t key0 = w * 32;
         uint32_t m = key0 >= nkeys ? 0u : (nkeys - key0 >= 32 ? ~0u : ((1u << (nkeys - key0)) - 1u));
-        if (m) m &= ~neg[(k0 + key0) >> 5];  // k0 is a multiple of 64
+        if (m) {  // k0 is a multiple of 64
+            m &= ~neg[(k0 + key0) >> 5];
+            if (alive) m &= alive[(k0 + key0) >> 5];  // refuted by an earlier probe round
+        }
         kbits[w] = m;
     }
     lds_barrier();
@@ -200,10 +275,11 @@ __global__ void __launch_bounds__(1024) k_gather_ring(TileMap tm, PartGeom pg, u
                 const uint32_t b = b0 + u * nwaves;
                 const uint32_t r = r0 + lane * 4;
                 if (b < B && r < fillb[u]) {
-                    uint32_t fails = ~(rw[u] >> (r & 31)) & 0xFu;
+                    uint32_t fails = ~r_quad(rw[u], r) & 0xFu;
                     if (fillb[u] - r < 4) fails &= (1u << (fillb[u] - r)) - 1u;
                     if (fails) {
-                        // q = the last group with pref[q] <= r (pref non-decreasing, pref[0] = 0)
+                        // q = the last group with pref[q] <= r (pref non-decreasing, pref[0] = 0);
+                        // a fixed-trip binary search keeps the wave's lanes together
                         const uint16_t* pb = lpref + b * nqs;
                         uint32_t lo = 0, len = nqs;
                         while (len > 1) {

@@ -400,15 +400,26 @@ __global__ void __launch_bounds__(256) k_ovf_build(TileMap tm, const uint32_t* _
 }
 
 // ------------------------------------------------------------------ probe: tiles
-// One workgroup per tile.  A work item is one 32-entry word of one region: 8 16-byte loads,
-// 32 LDS bit tests, one 4-byte store of result bits into R[(g*B + b)*(cap/32) + word].  Each
-// thread issues two work items' loads before testing either.  `expand` = the LDS budget allows
-// a per-word region id table (else a binary search over the word prefix).
+// Result bits R: one 32-bit word per 32-entry word of a region, bit (8t + l) = entry 4l + t
+// (l = the entry's 16-byte piece of the word, t = its place in the piece).  This is the layout
+// four wave ballots produce when 8 lanes read a word piece by piece (k_tile_probe).
+// r_quad: the 4 result bits of the piece holding entries r..r+3 (r % 4 == 0).
+__device__ __forceinline__ uint32_t r_quad(uint32_t rw, uint32_t r) {
+    const uint32_t l = (r & 31) >> 2;
+    return ((rw >> l) & 1u) | (((rw >> (8 + l)) & 1u) << 1) | (((rw >> (16 + l)) & 1u) << 2) |
+           (((rw >> (24 + l)) & 1u) << 3);
+}
+
+// One workgroup per tile.  Region words are read 8 per wave instruction: lane = one 16-byte
+// piece of a word, so an instruction reads 1 KiB contiguously (words are consecutive within a
+// region).  Each lane tests its 4 entries in the LDS tile; four ballots give every word's 32
+// result bits, stored by the word's first lane.  `expand` = the LDS budget allows a per-word
+// region id table (else a binary search over the word prefix).
 __global__ void __launch_bounds__(1024) k_tile_probe(TileMap tm, PartGeom pg, const uint32_t* __restrict__ regions,
                                                      const uint32_t* __restrict__ fill,
                                                      const uint32_t* __restrict__ bitmap, uint32_t* __restrict__ R,
                                                      int expand) {
-    extern __shared__ uint32_t smem[];
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     const uint32_t B = tm.nbuckets, G = pg.G, cap = pg.cap, wpr = cap / 32;
     const uint32_t b = blockIdx.x;
     const uint32_t W = 1u << (tm.tb - 5);
@@ -432,39 +443,39 @@ __global__ void __launch_bounds__(1024) k_tile_probe(TileMap tm, PartGeom pg, co
     lds_barrier();
     const uint32_t lmask = (1u << tm.tb) - 1u;
     const uint32_t total = wpre[G];
-    constexpr int U = 2;
-    for (uint32_t c0 = tid; c0 < total; c0 += nt * U) {
-        uint4 v[U][8];
+    const uint32_t lane = tid & 63, wave = tid >> 6, nwaves = nt >> 6;
+    const uint32_t l = lane & 7, wsub = lane >> 3;  // piece of the word, word of the instruction
+    const uint32_t stride = nwaves * 8;
+    constexpr int U = 8;  // instructions (8 words each) in flight per wave
+    for (uint32_t c0 = wave * 8; c0 < total; c0 += stride * U) {
+        uint4 v[U];
         uint32_t qq[U], word[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const uint32_t c = min(c0 + u * nt, total - 1);  // unconditional loads stay in registers
+            const uint32_t c = min(c0 + u * stride + wsub, total - 1);  // unconditional loads
             qq[u] = expand ? uint32_t(wq[c]) : bucket_of(wpre, G, c);
             word[u] = c - wpre[qq[u]];
-            const uint4* src = reinterpret_cast<const uint4*>(regions + (uint64_t(qq[u]) * B + b) * cap + word[u] * 32);
-#pragma unroll
-            for (int t = 0; t < 8; ++t) v[u][t] = src[t];
+            v[u] = reinterpret_cast<const uint4*>(regions + (uint64_t(qq[u]) * B + b) * cap + word[u] * 32)[l];
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const uint32_t c = c0 + u * nt;
-            if (c < total) {
-                const uint32_t f = fills[qq[u]];
-                const uint32_t e0 = word[u] * 32;
-                uint32_t bits = 0;
-#pragma unroll
-                for (int t = 0; t < 8; ++t) {
-                    uint32_t p = v[u][t].x & lmask;
-                    bits |= ((tile[p >> 5] >> (p & 31)) & 1u) << (t * 4);
-                    p = v[u][t].y & lmask;
-                    bits |= ((tile[p >> 5] >> (p & 31)) & 1u) << (t * 4 + 1);
-                    p = v[u][t].z & lmask;
-                    bits |= ((tile[p >> 5] >> (p & 31)) & 1u) << (t * 4 + 2);
-                    p = v[u][t].w & lmask;
-                    bits |= ((tile[p >> 5] >> (p & 31)) & 1u) << (t * 4 + 3);
-                }
-                if (f - e0 < 32) bits &= (1u << (f - e0)) - 1u;  // entries past the fill
-                R[(uint64_t(qq[u]) * B + b) * wpr + word[u]] = bits;
+            const uint32_t c = c0 + u * stride + wsub;
+            const uint32_t e = word[u] * 32 + l * 4;
+            const uint32_t lim = c < total ? fills[qq[u]] : 0u;  // entries past the fill read as 0
+            uint32_t p = v[u].x & lmask;
+            const bool t0 = (e < lim) & bool((tile[p >> 5] >> (p & 31)) & 1u);
+            p = v[u].y & lmask;
+            const bool t1 = (e + 1 < lim) & bool((tile[p >> 5] >> (p & 31)) & 1u);
+            p = v[u].z & lmask;
+            const bool t2 = (e + 2 < lim) & bool((tile[p >> 5] >> (p & 31)) & 1u);
+            p = v[u].w & lmask;
+            const bool t3 = (e + 3 < lim) & bool((tile[p >> 5] >> (p & 31)) & 1u);
+            const uint64_t m0 = __ballot(t0), m1 = __ballot(t1), m2 = __ballot(t2), m3 = __ballot(t3);
+            if (l == 0 && c < total) {
+                const uint32_t sh = wsub * 8;
+                R[(uint64_t(qq[u]) * B + b) * wpr + word[u]] =
+                    uint32_t((m0 >> sh) & 0xFF) | (uint32_t((m1 >> sh) & 0xFF) << 8) |
+                    (uint32_t((m2 >> sh) & 0xFF) << 16) | (uint32_t((m3 >> sh) & 0xFF) << 24);
             }
         }
     }
@@ -547,7 +558,7 @@ __global__ void __launch_bounds__(1024) k_gather(TileMap tm, PartGeom pg, uint64
                 const uint32_t b = b0 + u * nwaves;
                 const uint32_t r = r0 + lane * 4;
                 if (b < B && r < fillb[u]) {
-                    uint32_t fails = ~(rw[u] >> (r & 31)) & 0xFu;
+                    uint32_t fails = ~r_quad(rw[u], r) & 0xFu;
                     if (fillb[u] - r < 4) fails &= (1u << (fillb[u] - r)) - 1u;
                     if (fails) {
                         // sub-chunk of position r: the last j with pref[b][j] <= r

@@ -377,15 +377,15 @@ print('ok')
 """
 
 
-@pytest.mark.parametrize("part", ["sort", "ring"])
-def test_tiled_partition_strategies_and_region_overflow(part):
-    """Both partition passes of the tiled build / probe (PBF_PART forces one), with a key
-    repeated enough to overflow its tiles' regions and rings (build overflow list, probe
-    in-place test)."""
+@pytest.mark.parametrize("part,rounds", [("sort", "1"), ("ring", "1"), ("ring", "2")])
+def test_tiled_partition_strategies_and_region_overflow(part, rounds):
+    """Both partition passes of the tiled build / probe (PBF_PART forces one), the one- and
+    two-round tiled probe (PBF_PROBE_ROUNDS), with a key repeated enough to overflow its tiles'
+    regions and rings (build overflow list, probe in-place test)."""
     import os
     import subprocess
     import sys
-    env = dict(os.environ, PBF_PART=part)
+    env = dict(os.environ, PBF_PART=part, PBF_PROBE_ROUNDS=rounds)
     r = subprocess.run([sys.executable, "-c", _PART_CHILD], env=env, capture_output=True, text=True, timeout=600,
                        cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]

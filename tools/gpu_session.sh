@@ -32,6 +32,9 @@ for step in "$@"; do
          run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline
          run pmc_tcc 600 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum --output-format csv -d gpurun_out/pmc_tcc -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
     micro) run micro 300 tools/microbench/lds_rates ;;
+    variants) for v in build/variants/*.so; do nm=$(basename $v .so); PBF_LIB=$PWD/$v run var_$nm 300 python bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-host-inclusive; done
+              run var_default 300 python bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-host-inclusive ;;
+    rphases) run rphases 300 tools/microbench/ring_phases ;;
     phases) run phases_t0 300 tools/microbench/part_phases 0
             run phases_t16 300 tools/microbench/part_phases 16 ;;
     gapdiag) run native0 120 tools/microbench/pipeline_bench 50 0
