@@ -23,6 +23,9 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
+# per-pass HBM bytes from rocprofv3 PMC passes of this same bench (tools/traffic_summary.py);
+# used only when it was measured on the very library this run loads (sha256 match)
+TRAFFIC_FILE = os.path.join(REPO, "profiles", "traffic_{config}.json")
 
 CONFIGS = {
     # name: (n_build, nb_bytes, k, key kind)
@@ -58,6 +61,22 @@ def algorithmic_bytes(n, L, k, m_bits, offsets):
 
 def probe_bytes(n, L, k, offsets):
     return n * L + 4 * n * k + n // 8 + (8 * n if offsets else 0)
+
+
+def measured_traffic(config: str, lib_path: str) -> dict | None:
+    """{"build": bytes, "probe": bytes, "source": ...} from the committed PMC summary, or None
+    when there is none for this config or it was taken on a different libpebblebloom.so."""
+    import hashlib
+    path = TRAFFIC_FILE.format(config=config)
+    if not os.path.exists(path):
+        return None
+    t = json.load(open(path))
+    sha = hashlib.sha256(open(lib_path, "rb").read()).hexdigest()
+    if t.get("lib_sha256") != sha:
+        return None
+    out = {p: v["traffic_bytes"] for p, v in t["passes"].items()}
+    out["source"] = os.path.relpath(path, REPO) + ": " + t["source"] + "; " + t["correction"]
+    return out
 
 
 def cpu_baseline(nb_bytes, k, kind, budget_s):
@@ -290,6 +309,8 @@ def main():
         else:
             dom = {"kernel": ("probe pass (tiled: k_part<probe>+k_tile_probe+k_gather)" if bf.last_probe_mode == 2
                               else "k_probe"), "achieved": ach_probe, "ms": probe_ms, "bytes": b_probe}
+        traffic = measured_traffic(args.config, _native.lib_path())
+        dom_pass = "build" if build_ms >= probe_ms else "probe"
         out = {
             "metric": "Mkeys/s bloom build+probe (device-resident), 10M 16B keys; 1/2/4/8 GPU",
             "value": round(value, 3),
@@ -317,12 +338,14 @@ def main():
             "build_mode": bf.last_build_mode,
             "probe_mode": bf.last_probe_mode,
             "roofline": {"bound": "hbm", "achieved": round(dom["achieved"], 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(dom["achieved"] / HBM_PEAK_GBS, 4), "traffic": None, "kernel": dom["kernel"],
+                         "frac": round(dom["achieved"] / HBM_PEAK_GBS, 4),
+                         "traffic": int(traffic[dom_pass]) if traffic else None, "kernel": dom["kernel"],
                          "algorithmic_bytes": int(dom["bytes"]), "avg_ms": round(dom["ms"], 4)},
             "roofline_build": {"achieved": round(ach_build, 1), "frac": round(ach_build / HBM_PEAK_GBS, 4),
-                               "algorithmic_bytes": int(b_build)},
+                               "algorithmic_bytes": int(b_build), "traffic": int(traffic["build"]) if traffic else None},
             "roofline_probe": {"achieved": round(ach_probe, 1), "frac": round(ach_probe / HBM_PEAK_GBS, 4),
-                               "algorithmic_bytes": int(b_probe)},
+                               "algorithmic_bytes": int(b_probe), "traffic": int(traffic["probe"]) if traffic else None},
+            "traffic_source": traffic["source"] if traffic else "no PMC summary for this library build",
             "check": {"members_all_hit": members_ok, "false_positives": fp, "probes_absent": n},
         }
         if host_inc is not None:

@@ -85,6 +85,11 @@ def lib():
     return L
 
 
+def lib_path() -> str:
+    """Path of the loaded libpebblebloom.so (PBF_LIB overrides, for A/B builds)."""
+    return LIB_PATH
+
+
 def check(rc: int, what: str = "") -> None:
     if rc == PBF_OK:
         return

@@ -1,0 +1,91 @@
+"""HBM traffic per pass from rocprofv3 PMC passes (tools/gpu_session.sh step `traffic`).
+
+    python tools/traffic_summary.py FETCH_DIR WRITE_DIR OUT.json [--config c2]
+
+FETCH_SIZE and WRITE_SIZE come from separate `--pmc` runs of the same short bench (one counter
+group per run: FETCH_SIZE uses 3 of the 4 TCC slots, WRITE_SIZE 2).  Both are in KiB.  Per
+MI355X_MICROARCH.md §HBM, on gfx950 FETCH_SIZE reports exactly half the bytes of a wide
+(16 B/lane) streaming read, so fetched bytes = 2 x FETCH_SIZE x 1024; WRITE_SIZE is exact for
+16-B-per-lane stores.  Every kernel of the bloom passes reads its streams 16 B per lane
+(keys, region entries); the random word reads of the probe's spill path are negligible.
+
+Per kernel the median over dispatches of the full-size launches is taken; a pass's traffic is
+the sum over its kernels.  bench.py reads OUT.json to fill `roofline.traffic`.
+"""
+from __future__ import annotations
+
+import collections
+import csv
+import json
+import sys
+
+PASSES = {
+    "build": ("k_part_ring<", "false", "k_part<", "k_tile_build", "k_ovf_build"),
+    "probe": ("k_part_ring<", "true", "k_part<", "k_tile_probe", "k_gather"),
+}
+
+
+def per_kernel(path: str, counter: str) -> dict[str, float]:
+    vals = collections.defaultdict(list)
+    for r in csv.DictReader(open(f"{path}/run_counter_collection.csv")):
+        if r["Counter_Name"] != counter:
+            continue
+        name = r["Kernel_Name"].split("(")[0].replace("void ", "").strip()
+        vals[name].append(float(r["Counter_Value"]))
+    # full-size launches: the upper half of the dispatches by counter value
+    out = {}
+    for k, v in vals.items():
+        v = sorted(v)
+        out[k] = v[len(v) // 2] if len(v) < 3 else v[(3 * len(v)) // 4]
+    return out
+
+
+def pass_of(kernel: str) -> str | None:
+    if not kernel.startswith("pbf::"):
+        return None
+    if kernel.startswith("pbf::k_part"):
+        # k_part<KMAX, KM, PROBE> / k_part_ring<KMAX, KM, PROBE, POW2>
+        args = kernel[kernel.index("<") + 1:].rstrip(">").split(",")
+        return "probe" if args[2].strip() == "true" else "build"
+    if kernel in ("pbf::k_tile_build", "pbf::k_ovf_build"):
+        return "build"
+    if kernel in ("pbf::k_tile_probe", "pbf::k_gather", "pbf::k_gather_ring"):
+        return "probe"
+    return None
+
+
+def main() -> None:
+    fdir, wdir, out = sys.argv[1:4]
+    config = sys.argv[sys.argv.index("--config") + 1] if "--config" in sys.argv else "c2"
+    fetch = per_kernel(fdir, "FETCH_SIZE")
+    write = per_kernel(wdir, "WRITE_SIZE")
+    res = {"config": config, "source": f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE ({fdir}, {wdir})",
+           "correction": "read bytes = 2 x FETCH_SIZE x 1024 (gfx950 wide-read halving), write bytes = WRITE_SIZE x 1024",
+           "kernels": {}, "passes": {}}
+    for k in sorted(set(fetch) | set(write)):
+        p = pass_of(k)
+        if p is None:
+            continue
+        rd = 2.0 * fetch.get(k, 0.0) * 1024
+        wr = write.get(k, 0.0) * 1024
+        res["kernels"][k] = {"pass": p, "read_bytes": rd, "write_bytes": wr}
+        agg = res["passes"].setdefault(p, {"read_bytes": 0.0, "write_bytes": 0.0})
+        agg["read_bytes"] += rd
+        agg["write_bytes"] += wr
+    for p in res["passes"].values():
+        p["traffic_bytes"] = p["read_bytes"] + p["write_bytes"]
+    # the library these counters were taken on (bench.py only uses a summary of its own build)
+    import hashlib
+    import os
+    lib = os.environ.get("PBF_LIB") or os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                                   "pebbledb_amd", "libpebblebloom.so")
+    res["lib_sha256"] = hashlib.sha256(open(lib, "rb").read()).hexdigest()
+    json.dump(res, open(out, "w"), indent=1)
+    for k, v in res["kernels"].items():
+        print(f"{k:45s} {v['pass']:6s} read {v['read_bytes'] / 1e6:9.1f} MB  write {v['write_bytes'] / 1e6:9.1f} MB")
+    for p, v in res["passes"].items():
+        print(f"pass {p}: {v['traffic_bytes'] / 1e6:.1f} MB")
+
+
+if __name__ == "__main__":
+    main()
