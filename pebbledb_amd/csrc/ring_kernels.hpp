@@ -11,15 +11,16 @@
 // and a flush phase writes every complete GS-entry group (64 B at GS = 16) with ONE wave store
 // instruction (4 lanes x 16 B), so each region line leaves as whole 64-B requests.
 //
-//   ring      RC entries per tile (RC = 2*GS).  head[b] = entries flushed (= the region write
-//             cursor, a multiple of GS), tail[b] = entries appended.  Entry e of tile b sits at
+//   ring      RC entries per tile (RC = 2*GS).  head = entries flushed (= the region write
+//             cursor, a multiple of GS), tail = entries appended; packed in one u64 per tile.  Entry e of tile b sits at
 //             ring[b*RC + (e % RC)] and lands at region position e.
 //   sub-chunk 1024 keys (one per thread).  The host picks the geometry so a tile receives ~GS/3
 //             positions per sub-chunk; a position that would overrun the ring (or the region
 //             capacity) leaves the stream like k_part's overflow (build: overflow list; probe:
 //             tested against the bitmap in place, a miss clears the key via `neg`).
 //   probe     entry = (j & 3) << 30 | slot << 20 | position-in-tile (slot = thread, j = sub-chunk).
-//             pref[g][q][b] = in-region entries of (g, b) before sub-chunk 4q, so k_gather_ring
+//             pref[g][q][b] = in-region entries of (g, b) before sub-chunk 4q (b fastest, so a
+//             wave's stores of 64 tiles are one contiguous 256-B run), so k_gather_ring
 //             finds an entry's sub-chunk from its region position and the entry's j & 3.
 //   rounds    The probe runs in two rounds, the batched form of may_contain's early exit
 //             (bloom_filter.py:71-73): round 1 tests seed 0 of every key; round 2 tests seeds
@@ -64,14 +65,15 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
     const uint32_t g = blockIdx.x;
     const uint32_t cap = pg.cap;
     const uint32_t lmask = (1u << tm.tb) - 1u;
-    uint32_t* head = smem;                                   // B
-    uint32_t* tail = head + B;                               // B
-    uint32_t* desc = tail + B;                               // 16 waves x 128 group descriptors
+    // ht[b] = head << 32 | tail: one 64-bit LDS atomic add appends a position and returns the
+    // tile's flush cursor with its slot (no separate head read per position)
+    unsigned long long* ht = reinterpret_cast<unsigned long long*>(smem);  // B
+    uint32_t* desc = smem + 2 * B;                           // 16 waves x 128 group descriptors
     uint32_t* ring = smem + ((2 * B + 16 * 128 + 3) & ~3u);  // B * RC, 16-B aligned
     const uint32_t nqs = pg.nq + 1;  // pref entries per (g, b)
     for (uint32_t b = tid; b < B; b += nt) {
-        head[b] = tail[b] = 0;
-        if constexpr (PROBE) pref[(uint64_t(g) * B + b) * nqs] = 0;
+        ht[b] = 0;
+        if constexpr (PROBE) pref[uint64_t(g) * nqs * B + b] = 0;
     }
     const uint64_t k0 = uint64_t(g) * pg.kpw;
     const uint64_t k1 = min(n, k0 + pg.kpw);
@@ -128,8 +130,9 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
 #pragma unroll
                 for (int s = 0; s < KMAX; ++s) {
                     if (s < k) {
-                        slot[s] = atomicAdd(tail + (pos[s] >> tm.tb), 1u);
-                        hd[s] = head[pos[s] >> tm.tb];
+                        const unsigned long long v = atomicAdd(ht + (pos[s] >> tm.tb), 1ull);
+                        slot[s] = uint32_t(v);
+                        hd[s] = uint32_t(v >> 32);
                     }
                 }
                 PBF_STAMP(2);
@@ -170,11 +173,11 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
             const uint32_t gpi = 64 / lpg;  // groups per store instruction
             for (uint32_t b0 = wave * 64; b0 < B; b0 += nt) {
                 const uint32_t b = b0 + lane;
-                uint32_t ng = 0, h = 0;
+                uint32_t ng = 0, h = 0, t = 0;
                 if (b < B) {
-                    h = head[b];
-                    const uint32_t t = min(tail[b], min(h + RC, cap));  // positions past these left the stream
-                    tail[b] = t;
+                    const unsigned long long hv = ht[b];
+                    h = uint32_t(hv >> 32);
+                    t = min(uint32_t(hv), min(h + RC, cap));  // positions past these left the stream
                     ng = (t - h) / GS;
                 }
                 const uint64_t m1 = __ballot(ng >= 1), m2 = __ballot(ng >= 2);
@@ -196,23 +199,47 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
                 }
                 __builtin_amdgcn_wave_barrier();
                 if (b < B) {
-                    head[b] = h + ng * GS;
+                    ht[b] = (uint64_t(h + ng * GS) << 32) | t;
                     if constexpr (PROBE)
-                        if (((j + 1) & 3) == 0) pref[(uint64_t(g) * B + b) * nqs + ((j + 1) >> 2)] = tail[b];
+                        if (((j + 1) & 3) == 0) pref[(uint64_t(g) * nqs + ((j + 1) >> 2)) * B + b] = t;
                 }
             }
             PBF_STAMP(5);
         }
     }
     lds_barrier();
-    // the last partial group of every tile, and the fill counts
+    // The last partial group of every tile leaves as a whole group too (entries past the fill
+    // count are never read; the region has room: head is a multiple of GS and cap of 32).
+    {
+        uint32_t* wd = desc + wave * 128;
+        const uint32_t lpg = GS / 4, gpi = 64 / lpg;
+        for (uint32_t b0 = wave * 64; b0 < B; b0 += nt) {
+            const uint32_t b = b0 + lane;
+            const unsigned long long hv = b < B ? ht[b] : 0ull;
+            const bool part = uint32_t(hv) > uint32_t(hv >> 32);
+            const uint64_t m1 = __ballot(part);
+            const uint32_t at = __popcll(m1 & ((uint64_t(1) << lane) - 1)), total = __popcll(m1);
+            if (part) wd[at] = b | (uint32_t(hv >> 32) << 12);
+            __builtin_amdgcn_wave_barrier();
+            for (uint32_t c = 0; c < total; c += gpi) {
+                const uint32_t gi = c + lane / lpg, q = lane % lpg;
+                if (gi < total) {
+                    const uint32_t d = wd[gi];
+                    const uint32_t tb = d & 0xFFFu;
+                    const uint32_t e = (d >> 12) + q * 4;
+                    const uint4 v = *reinterpret_cast<const uint4*>(ring + tb * RC + (e & rmask));
+                    *reinterpret_cast<uint4*>(regions + (uint64_t(g) * B + tb) * cap + e) = v;
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+    // fill counts; the probe's remaining cumulative counts
     for (uint32_t b = tid; b < B; b += nt) {
-        const uint32_t h = head[b], t = tail[b];
-        uint32_t* dst = regions + (uint64_t(g) * B + b) * cap;
-        for (uint32_t e = h; e < t; ++e) dst[e] = ring[b * RC + (e & rmask)];
+        const uint32_t t = uint32_t(ht[b]);
         fill[uint64_t(b) * pg.G + g] = t;
         if constexpr (PROBE)
-            for (uint32_t q = (j + 3) >> 2; q <= pg.nq; ++q) pref[(uint64_t(g) * B + b) * nqs + q] = t;
+            for (uint32_t q = (j + 3) >> 2; q <= pg.nq; ++q) pref[(uint64_t(g) * nqs + q) * B + b] = t;
     }
 }
 
@@ -239,8 +266,8 @@ __global__ void __launch_bounds__(1024) k_gather_ring(TileMap tm, PartGeom pg, u
     const uint32_t kw = uint32_t((pg.kpw + 31) / 32);
     uint32_t* kbits = smem;                                    // kw words
     uint16_t* lpref = reinterpret_cast<uint16_t*>(kbits + kw);  // B * nqs (values <= cap < 2^16)
-    const uint32_t* gp = pref + uint64_t(g) * B * nqs;
-    for (uint32_t x = tid; x < B * nqs; x += nt) lpref[x] = uint16_t(gp[x]);
+    const uint32_t* gp = pref + uint64_t(g) * nqs * B;  // [q][b] in memory, [b][q] in LDS
+    for (uint32_t x = tid; x < B * nqs; x += nt) lpref[(x % B) * nqs + x / B] = uint16_t(gp[x]);
     for (uint32_t w = tid; w < kw; w += nt) {
         const uint32_t key0 = w * 32;
         uint32_t m = key0 >= nkeys ? 0u : (nkeys - key0 >= 32 ? ~0u : ((1u << (nkeys - key0)) - 1u));
