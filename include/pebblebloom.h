@@ -79,6 +79,20 @@ int pbf_probe_fixed(pbf_filter_t* f, const uint8_t* keys, uint32_t key_len, uint
 int pbf_probe(pbf_filter_t* f, const uint8_t* keys, const uint64_t* offsets, uint64_t n, uint8_t* hitmask,
               int keys_on_device);
 
+/* LsmStorage.get's filter checks for a batch of keys against several SSTable filters
+ * (src/lsm_storage.py:164-169 L0 newest-first, :173-175 per level): hitmasks[i] receives
+ * may_contain over the batch for filters[i], ceil(n/8) bytes LSB-first, host or device memory as
+ * keys_on_device says (hitmasks itself is a host array of nfilters pointers).  All filters
+ * must be on one device and distinct.  When they share (nb_bytes, k) -- one SSTable size class,
+ * the usual case -- the keys are hashed and partitioned once for up to 8 filters and only the
+ * tile test and gather run per filter; otherwise each filter is probed on its own stream.  With
+ * keys_on_device = 1 the call is asynchronous on filters[0]'s stream (pbf_sync(filters[0]));
+ * every other filter's stream is ordered before and after it. */
+int pbf_probe_multi_fixed(pbf_filter_t* const* filters, uint32_t nfilters, const uint8_t* keys, uint32_t key_len,
+                          uint64_t n, uint8_t* const* hitmasks, int keys_on_device);
+int pbf_probe_multi(pbf_filter_t* const* filters, uint32_t nfilters, const uint8_t* keys, const uint64_t* offsets,
+                    uint64_t n, uint8_t* const* hitmasks, int keys_on_device);
+
 /* The k bit indices of each key, BloomFilter._hash (bloom_filter.py:38-49): out[i*k + s] =
  * mmh3.hash(key_i, s) % bits_size (Python floor-mod).  out is host or device memory as
  * keys_on_device says (n*k uint64).  Used for index-math parity at any m. */

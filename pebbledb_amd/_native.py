@@ -37,6 +37,8 @@ SIGNATURES = {
     "pbf_add": (_int, [_vp, _u8p, _vp, _u64, _int]),
     "pbf_probe_fixed": (_int, [_vp, _u8p, _u32, _u64, _u8p, _int]),
     "pbf_probe": (_int, [_vp, _u8p, _vp, _u64, _u8p, _int]),
+    "pbf_probe_multi_fixed": (_int, [_vp, _u32, _u8p, _u32, _u64, _vp, _int]),
+    "pbf_probe_multi": (_int, [_vp, _u32, _u8p, _vp, _u64, _vp, _int]),
     "pbf_hash_indices_fixed": (_int, [_vp, _u8p, _u32, _u64, _vp, _int]),
     "pbf_hash_indices": (_int, [_vp, _u8p, _vp, _u64, _vp, _int]),
     "pbf_get_bitmap": (_int, [_vp, _u8p, _u64]),

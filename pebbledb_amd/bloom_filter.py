@@ -289,3 +289,66 @@ class BloomFilter:
 
     def __repr__(self):
         return f"BloomFilter(nb_bytes={self.nb_bytes}, nb_hash_functions={self.nb_hash_functions}, device={self.device})"
+
+
+# ---------------------------------------------------------------------- multi-filter probe
+def _native_set(filters):
+    """Split `filters` into the ones the native multi-probe takes (a device handle, k > 0) and
+    the host-decided rest (k == 0: always True; nb_bytes == 0: ZeroDivisionError, as
+    bloom_filter.py:47 raises)."""
+    native = []
+    for i, bf in enumerate(filters):
+        if bf._require_modulus():
+            bf._flush()
+            native.append(i)
+    return native
+
+
+def may_contain_multi(filters, keys) -> np.ndarray:
+    """``may_contain`` of every key against every filter, the batched form of
+    ``LsmStorage.get``'s filter checks (src/lsm_storage.py:164-175).  Returns a uint8 matrix
+    [len(filters), ceil(n/8)] of LSB-first hit masks.  Filters must share a device; when they
+    also share (nb_bytes, k) the keys are hashed and partitioned once (pbf_probe_multi)."""
+    filters = list(filters)
+    pk = keys if isinstance(keys, PackedKeys) else PackedKeys.from_strs(list(keys))
+    nbm = (pk.n + 7) // 8
+    out = np.zeros((len(filters), nbm), dtype=np.uint8)
+    if pk.n == 0 or not filters:
+        return out
+    native = _native_set(filters)
+    for i in set(range(len(filters))) - set(native):
+        out[i, :] = 0xFF
+        if pk.n % 8:
+            out[i, -1] = (1 << (pk.n % 8)) - 1
+    if native:
+        hs = (ctypes.c_void_p * len(native))(*[filters[i]._h.value for i in native])
+        outs = (ctypes.c_void_p * len(native))(*[out[i].ctypes.data for i in native])
+        L = _native.lib()
+        if pk.key_len > 0:
+            rc = L.pbf_probe_multi_fixed(hs, len(native), _vp(pk.data), pk.key_len, pk.n, outs, 0)
+        else:
+            rc = L.pbf_probe_multi(hs, len(native), _vp(pk.data), _vp(pk.offsets), pk.n, outs, 0)
+        _native.check(rc, "pbf_probe_multi")
+    return out
+
+
+def probe_multi_device(filters, keys_ptr: int, n: int, hitmask_ptrs, key_len: int = 0, offsets_ptr: int = 0) -> None:
+    """Device-resident multi-filter probe: keys (fixed key_len, or offsets) and the hit masks are
+    device pointers on the filters' device; asynchronous on filters[0].stream (filters[0].sync())."""
+    filters = list(filters)
+    if n == 0 or not filters:
+        return
+    if len(hitmask_ptrs) != len(filters):
+        raise ValueError("one hit mask per filter")
+    for bf in filters:
+        if not bf._require_modulus():
+            raise ValueError("probe_multi_device: k == 0 filters are decided on the host (may_contain_multi)")
+        bf._flush()
+    hs = (ctypes.c_void_p * len(filters))(*[bf._h.value for bf in filters])
+    outs = (ctypes.c_void_p * len(filters))(*[int(p) for p in hitmask_ptrs])
+    L = _native.lib()
+    if offsets_ptr:
+        rc = L.pbf_probe_multi(hs, len(filters), ctypes.c_void_p(keys_ptr), ctypes.c_void_p(offsets_ptr), n, outs, 1)
+    else:
+        rc = L.pbf_probe_multi_fixed(hs, len(filters), ctypes.c_void_p(keys_ptr), key_len, n, outs, 1)
+    _native.check(rc, "pbf_probe_multi")

@@ -19,6 +19,7 @@
 #include <mutex>
 #include <string>
 #include <type_traits>
+#include <vector>
 
 #include "../../include/pebblebloom.h"
 #include "bloom_kernels.hpp"
@@ -210,6 +211,7 @@ struct pbf_filter {
     PinBuf pin[2];
     int pin_next = 0;
     uint64_t* dpop = nullptr;
+    hipEvent_t ev = nullptr;  // stream joins of multi-filter probes
 };
 
 namespace {
@@ -382,14 +384,14 @@ int run_tiled(pbf_filter_t* f, const Batch& b) {
                     err = allow_lds(kern, pl.lds_part);
                     if (err == hipSuccess)
                         kern<<<pg.G, kPartThreads, pl.lds_part, s>>>(b.ks, b.n, int(k), tm, pg, regions, fill, nullptr,
-                                                             ovf, ovf_count, nullptr, nullptr, 0, nullptr);
+                                                             ovf, ovf_count, ProbeSet{}, 0, nullptr);
                 }
             } else {
                 auto kern = k_part<KX, KMD, false>;
                 err = allow_lds(kern, pl.lds_part);
                 if (err == hipSuccess)
                     kern<<<pg.G, kPartThreads, pl.lds_part, s>>>(b.ks, b.n, int(k), tm, pg, regions, fill, nullptr, ovf,
-                                                         ovf_count, nullptr, nullptr);
+                                                         ovf_count, ProbeSet{});
             }
         }
     });
@@ -405,7 +407,12 @@ int run_tiled(pbf_filter_t* f, const Batch& b) {
     return PBF_OK;
 }
 
-int run_tiled_probe(pbf_filter_t* f, const Batch& b, uint8_t* hitmask) {
+// Tiled probe of one key batch against nf filters sharing (m, k) (nf = 1: a plain probe).  The
+// keys are hashed and partitioned once, on fs[0]'s stream with fs[0]'s scratch; the tile test
+// and the gather then run once per filter.  hitmasks[i] + hm_off is filter i's output.
+int run_tiled_probe_set(pbf_filter_t* const* fs, uint32_t nf, const Batch& b, uint8_t* const* hitmasks,
+                        uint64_t hm_off) {
+    pbf_filter_t* f = fs[0];
     const TileMap& tm = f->tm;
     const uint32_t B = tm.nbuckets;
     const uint32_t k = f->k;
@@ -416,23 +423,29 @@ int run_tiled_probe(pbf_filter_t* f, const Batch& b, uint8_t* hitmask) {
     // sort partition: per-sub-chunk tile counts; ring partition: cumulative counts per 4 sub-chunks
     HIP_TRY(f->subcnt.ensure(pg.ring ? size_t(pg.G) * B * (pg.nq + 1) * 4 : size_t(pg.G) * pg.nsub * B * 4));
     HIP_TRY(f->rbits.ensure(size_t(pg.G) * B * (pg.cap / 32) * 4));
-    const size_t neg_bytes = ((b.n + 31) / 32) * 4;
-    HIP_TRY(f->neg.ensure(neg_bytes));
+    const uint64_t neg_words = (b.n + 31) / 32;
+    const size_t neg_bytes = neg_words * 4;
+    HIP_TRY(f->neg.ensure(neg_bytes * nf));
     auto* regions = static_cast<uint32_t*>(f->regions.p);
     auto* fill = static_cast<uint32_t*>(f->fill.p);
     auto* subcnt = static_cast<uint32_t*>(f->subcnt.p);
     auto* R = static_cast<uint32_t*>(f->rbits.p);
     auto* neg = static_cast<uint32_t*>(f->neg.p);
     hipStream_t s = f->stream;
+    ProbeSet ps{};
+    ps.nf = nf;
+    ps.neg = neg;
+    ps.neg_stride = neg_words;
+    for (uint32_t i = 0; i < nf; ++i) ps.bm[i] = fs[i]->bitmap;
     size_t lds_tile = ((size_t(1) << tm.tb) / 32 + 2 * pg.G + 1 + 16) * 4;
     const size_t lds_expand = size_t(pg.G) * (pg.cap / 32) * 2;
     const int expand = lds_tile + lds_expand <= 160 * 1024 ? 1 : 0;
     if (expand) lds_tile += lds_expand;
     HIP_TRY(allow_lds(k_tile_probe, lds_tile));
-    // One probe round: seeds [sbase, sbase + kr) of the keys `alive` marks (all if null), the
-    // round's hit mask (AND alive) into `out`.
-    auto round = [&](int sbase, uint32_t kr, const uint32_t* alive, uint8_t* out) -> int {
-        HIP_TRY(hipMemsetAsync(neg, 0, neg_bytes, s));
+    // One probe round: seeds [sbase, sbase + kr) of the keys `alive` marks (all if null), each
+    // filter's round hit mask (AND alive) into outs[i] + hm_off.
+    auto round = [&](int sbase, uint32_t kr, const uint32_t* alive, uint8_t* const* outs) -> int {
+        HIP_TRY(hipMemsetAsync(neg, 0, neg_bytes * nf, s));
         hipError_t err = hipSuccess;
         dispatch(kmax_for(kr), b.km, [&](auto KMAX, auto KM) {
             if constexpr (decltype(KMAX)::value > 0) {
@@ -443,38 +456,51 @@ int run_tiled_probe(pbf_filter_t* f, const Batch& b, uint8_t* hitmask) {
                         err = allow_lds(kern, pl.lds_part);
                         if (err == hipSuccess)
                             kern<<<pg.G, kPartThreads, pl.lds_part, s>>>(b.ks, b.n, int(kr), tm, pg, regions, fill,
-                                                                 subcnt, nullptr, nullptr, f->bitmap, neg, sbase, alive);
+                                                                 subcnt, nullptr, nullptr, ps, sbase, alive);
                     }
                 } else {
                     auto kern = k_part<KX, KMD, true>;
                     err = allow_lds(kern, pl.lds_part);
                     if (err == hipSuccess)
                         kern<<<pg.G, kPartThreads, pl.lds_part, s>>>(b.ks, b.n, int(kr), tm, pg, regions, fill, subcnt,
-                                                             nullptr, nullptr, f->bitmap, neg);
+                                                             nullptr, nullptr, ps);
                 }
             }
         });
         HIP_TRY(err);
         CHECK_LAUNCH();
-        k_tile_probe<<<B, 1024, lds_tile, s>>>(tm, pg, regions, fill, f->bitmap, R, expand);
-        CHECK_LAUNCH();
-        if (pg.ring) {
-            HIP_TRY(allow_lds(k_gather_ring, pl.lds_gather));
-            k_gather_ring<<<pg.G, 1024, pl.lds_gather, s>>>(tm, pg, b.n, regions, R, fill, subcnt, neg, alive, out);
-        } else {
-            HIP_TRY(allow_lds(k_gather, pl.lds_gather));
-            k_gather<<<pg.G, 1024, pl.lds_gather, s>>>(tm, pg, b.n, regions, R, subcnt, neg, out);
+        if (pg.ring) HIP_TRY(allow_lds(k_gather_ring, pl.lds_gather));
+        else HIP_TRY(allow_lds(k_gather, pl.lds_gather));
+        for (uint32_t i = 0; i < nf; ++i) {
+            k_tile_probe<<<B, 1024, lds_tile, s>>>(tm, pg, regions, fill, fs[i]->bitmap, R, expand);
+            CHECK_LAUNCH();
+            const uint32_t* negi = neg + i * neg_words;
+            if (pg.ring)
+                k_gather_ring<<<pg.G, 1024, pl.lds_gather, s>>>(tm, pg, b.n, regions, R, fill, subcnt, negi, alive,
+                                                               outs[i] + hm_off);
+            else
+                k_gather<<<pg.G, 1024, pl.lds_gather, s>>>(tm, pg, b.n, regions, R, subcnt, negi, outs[i] + hm_off);
+            CHECK_LAUNCH();
         }
-        CHECK_LAUNCH();
         return PBF_OK;
     };
-    if (!pg.ring || k < 2 || probe_rounds() < 2) return round(0, k, nullptr, hitmask);
+    if (nf > 1 || !pg.ring || k < 2 || probe_rounds() < 2) return round(0, k, nullptr, hitmasks);
     // two rounds: seed 0 for every key, then seeds 1..k-1 for the keys seed 0 left alive
     HIP_TRY(f->alive.ensure(neg_bytes));
     auto* alive = static_cast<uint32_t*>(f->alive.p);
-    int rc = round(0, 1, nullptr, reinterpret_cast<uint8_t*>(alive));
+    uint8_t* alive_out[1] = {reinterpret_cast<uint8_t*>(alive)};
+    const uint64_t keep_off = hm_off;
+    hm_off = 0;
+    int rc = round(0, 1, nullptr, alive_out);
     if (rc) return rc;
-    return round(1, k - 1, alive, hitmask);
+    hm_off = keep_off;
+    return round(1, k - 1, alive, hitmasks);
+}
+
+int run_tiled_probe(pbf_filter_t* f, const Batch& b, uint8_t* hitmask) {
+    pbf_filter_t* fs[1] = {f};
+    uint8_t* outs[1] = {hitmask};
+    return run_tiled_probe_set(fs, 1, b, outs, 0);
 }
 
 // The partition pass needs its tile counters plus a stage of one key per thread in LDS.
@@ -564,6 +590,75 @@ int probe_device(pbf_filter_t* f, const Batch& b, uint8_t* hitmask_dev) {
     });
     CHECK_LAUNCH();
     f->last_probe_mode = PBF_PROBE_DIRECT;
+    return PBF_OK;
+}
+
+// ---- multi-filter probe (LsmStorage.get over a key batch, src/lsm_storage.py:164-179) ----
+
+hipError_t filter_event(pbf_filter_t* f) {
+    if (f->ev) return hipSuccess;
+    return hipEventCreateWithFlags(&f->ev, hipEventDisableTiming);
+}
+
+// One pipeline serves the whole set when every filter has fs[0]'s (nb_bytes, k) and the tiled
+// probe is what fs[0] would pick for this batch (a filter pinned to the direct probe opts out).
+bool shared_probe(pbf_filter_t* const* fs, uint32_t nf, uint64_t n) {
+    for (uint32_t i = 1; i < nf; ++i)
+        if (fs[i]->nb_bytes != fs[0]->nb_bytes || fs[i]->k != fs[0]->k || fs[i]->probe_mode == PBF_PROBE_DIRECT)
+            return false;
+    return want_tiled_probe(fs[0], n);
+}
+
+// Device keys / hit masks; asynchronous on fs[0]'s stream.  Every other filter's stream first
+// hands its pending work (a build, a from_bytes) to fs[0]'s stream and afterwards waits for the
+// probe, so later calls on any handle are ordered after it.
+int probe_multi_device(pbf_filter_t* const* fs, uint32_t nf, const Batch& b, uint8_t* const* hitmasks) {
+    pbf_filter_t* f0 = fs[0];
+    hipStream_t s0 = f0->stream;
+    int rc = materialise(f0);
+    if (rc) return rc;
+    HIP_TRY(filter_event(f0));
+    const bool shared = shared_probe(fs, nf, b.n);
+    if (!shared) HIP_TRY(hipEventRecord(f0->ev, s0));  // keys ready on s0
+    for (uint32_t i = 1; i < nf; ++i) {
+        pbf_filter_t* fi = fs[i];
+        rc = materialise(fi);
+        if (rc) return rc;
+        HIP_TRY(filter_event(fi));
+        if (!shared) HIP_TRY(hipStreamWaitEvent(fi->stream, f0->ev, 0));
+    }
+    if (shared) {
+        for (uint32_t i = 1; i < nf; ++i) {
+            HIP_TRY(hipEventRecord(fs[i]->ev, fs[i]->stream));
+            HIP_TRY(hipStreamWaitEvent(s0, fs[i]->ev, 0));
+        }
+        const uint64_t per = tiled_probe_batch(f0, b.km);
+        for (uint64_t i0 = 0; i0 < b.n; i0 += per) {
+            Batch c = b;
+            c.n = std::min<uint64_t>(per, b.n - i0);
+            if (b.km == kVar)
+                c.ks.offsets = b.ks.offsets + i0;
+            else
+                c.ks.data = b.ks.data + i0 * b.ks.key_len;
+            for (uint32_t g0 = 0; g0 < nf; g0 += kMaxProbeSet) {
+                rc = run_tiled_probe_set(fs + g0, std::min<uint32_t>(kMaxProbeSet, nf - g0), c, hitmasks + g0, i0 / 8);
+                if (rc) return rc;
+            }
+        }
+        for (uint32_t i = 0; i < nf; ++i) fs[i]->last_probe_mode = PBF_PROBE_TILED;
+    } else {
+        // each filter on its own stream (and scratch), joined back into fs[0]'s
+        for (uint32_t i = 0; i < nf; ++i) {
+            rc = probe_device(fs[i], b, hitmasks[i]);
+            if (rc) return rc;
+        }
+        for (uint32_t i = 1; i < nf; ++i) {
+            HIP_TRY(hipEventRecord(fs[i]->ev, fs[i]->stream));
+            HIP_TRY(hipStreamWaitEvent(s0, fs[i]->ev, 0));
+        }
+    }
+    HIP_TRY(hipEventRecord(f0->ev, s0));
+    for (uint32_t i = 1; i < nf; ++i) HIP_TRY(hipStreamWaitEvent(fs[i]->stream, f0->ev, 0));
     return PBF_OK;
 }
 
@@ -701,6 +796,38 @@ int probe_impl(pbf_filter_t* f, const uint8_t* keys, const uint64_t* offsets, ui
     return PBF_OK;
 }
 
+int probe_multi_impl(pbf_filter_t* const* fs, uint32_t nf, const uint8_t* keys, const uint64_t* offsets,
+                     uint32_t key_len, uint64_t n, uint8_t* const* hitmasks, int on_device) {
+    if (nf == 0) return PBF_OK;
+    if (!fs || !hitmasks) return fail(PBF_ERR_INVALID, "null filter or hitmask array");
+    for (uint32_t i = 0; i < nf; ++i) {
+        if (!fs[i]) return fail(PBF_ERR_INVALID, "null filter handle in set");
+        if (fs[i]->device != fs[0]->device) return fail(PBF_ERR_INVALID, "filters of one multi-probe must share a device");
+        if (n && !hitmasks[i]) return fail(PBF_ERR_INVALID, "null hitmask in set");
+        for (uint32_t j = 0; j < i; ++j)
+            if (fs[j] == fs[i]) return fail(PBF_ERR_INVALID, "a filter appears twice in the set");
+    }
+    int rc = check_keys(fs[0], keys, offsets, key_len, n, offsets != nullptr);
+    if (rc || n == 0) return rc;
+    if (on_device) return probe_multi_device(fs, nf, make_batch(keys, offsets, key_len, n), hitmasks);
+    pbf_filter_t* f0 = fs[0];
+    std::vector<uint8_t*> douts(nf);
+    rc = for_host_chunks(f0, keys, offsets, key_len, n, 64, [&](const Batch& b, uint64_t i0) {
+        const size_t stride = (((b.n + 7) / 8) + 255) & ~size_t(255);
+        HIP_TRY(f0->dout.ensure(stride * nf + 8));
+        for (uint32_t i = 0; i < nf; ++i) douts[i] = static_cast<uint8_t*>(f0->dout.p) + i * stride;
+        int r = probe_multi_device(fs, nf, b, douts.data());
+        if (r) return r;
+        for (uint32_t i = 0; i < nf; ++i)
+            HIP_TRY(hipMemcpyAsync(hitmasks[i] + i0 / 8, douts[i], (b.n + 7) / 8, hipMemcpyDeviceToHost, f0->stream));
+        HIP_TRY(hipStreamSynchronize(f0->stream));
+        return PBF_OK;
+    });
+    if (rc) return rc;
+    HIP_TRY(hipStreamSynchronize(f0->stream));
+    return PBF_OK;
+}
+
 int hash_impl(pbf_filter_t* f, const uint8_t* keys, const uint64_t* offsets, uint32_t key_len, uint64_t n,
               uint64_t* out, int on_device) {
     int rc = check_keys(f, keys, offsets, key_len, n, offsets != nullptr);
@@ -814,6 +941,7 @@ int pbf_destroy(pbf_filter_t* f) {
     f->dout.release();
     f->pin[0].release();
     f->pin[1].release();
+    if (f->ev) (void)hipEventDestroy(f->ev);
     if (f->stream) (void)hipStreamDestroy(f->stream);
     delete f;
     return PBF_OK;
@@ -873,6 +1001,19 @@ int pbf_probe(pbf_filter_t* f, const uint8_t* keys, const uint64_t* offsets, uin
               int on_device) {
     if (!offsets && n > 0) return fail(PBF_ERR_INVALID, "null offsets");
     return probe_impl(f, keys ? keys : reinterpret_cast<const uint8_t*>(offsets), offsets, 0, n, hitmask, on_device);
+}
+
+int pbf_probe_multi_fixed(pbf_filter_t* const* filters, uint32_t nfilters, const uint8_t* keys, uint32_t key_len,
+                          uint64_t n, uint8_t* const* hitmasks, int on_device) {
+    if (key_len == 0 && n > 0) return fail(PBF_ERR_INVALID, "key_len 0: use pbf_probe_multi with offsets");
+    return probe_multi_impl(filters, nfilters, keys, nullptr, key_len, n, hitmasks, on_device);
+}
+
+int pbf_probe_multi(pbf_filter_t* const* filters, uint32_t nfilters, const uint8_t* keys, const uint64_t* offsets,
+                    uint64_t n, uint8_t* const* hitmasks, int on_device) {
+    if (!offsets && n > 0) return fail(PBF_ERR_INVALID, "null offsets");
+    return probe_multi_impl(filters, nfilters, keys ? keys : reinterpret_cast<const uint8_t*>(offsets), offsets, 0, n,
+                            hitmasks, on_device);
 }
 
 int pbf_hash_indices_fixed(pbf_filter_t* f, const uint8_t* keys, uint32_t key_len, uint64_t n, uint64_t* out,

@@ -55,8 +55,7 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
                                                     uint32_t* __restrict__ regions, uint32_t* __restrict__ fill,
                                                     uint32_t* __restrict__ pref, uint32_t* __restrict__ ovf,
                                                     uint32_t* __restrict__ ovf_count,
-                                                    const uint32_t* __restrict__ bitmap, uint32_t* __restrict__ neg,
-                                                    int sbase, const uint32_t* __restrict__ alive) {
+                                                    ProbeSet ps, int sbase, const uint32_t* __restrict__ alive) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     const uint32_t B = tm.nbuckets;
     const uint32_t RC = pg.ring, GS = RC / 2, rmask = RC - 1;
@@ -153,8 +152,7 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
                     for (int s = 0; s < KMAX; ++s) {
                         if ((spill >> s) & 1u) {
                             if constexpr (PROBE) {  // test this position here
-                                const uint64_t bit = pos_to_bit(pos[s], tm);
-                                if (!((bitmap[bit >> 5] >> (bit & 31)) & 1u)) atomicOr(neg + (i >> 5), 1u << (i & 31));
+                                spill_probe(ps, pos_to_bit(pos[s], tm), i);
                             } else {
                                 ovf[atomicAdd(ovf_count, 1u)] = pos[s];
                             }

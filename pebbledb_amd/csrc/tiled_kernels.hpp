@@ -44,6 +44,25 @@ struct TileMap {
     uint64_t total_words;  // ceil(nb_bytes / 4)
 };
 
+// The bitmaps a probe partition tests its overflowed (spilled) entries against: one per filter
+// of a multi-filter probe (pbf_probe_multi, all with the same m and k); filter f's misses clear
+// key bits in neg + f * neg_stride.  A build passes nf = 0.
+constexpr int kMaxProbeSet = 8;
+struct ProbeSet {
+    const uint32_t* bm[kMaxProbeSet];
+    uint32_t* neg;
+    uint64_t neg_stride;  // u32 words
+    uint32_t nf;
+    uint32_t pad;
+};
+
+// A spilled probe entry: test bit `bit` in every filter of the set, clear `key` where it is 0.
+__device__ __forceinline__ void spill_probe(const ProbeSet& ps, uint64_t bit, uint64_t key) {
+    for (uint32_t f = 0; f < ps.nf; ++f)
+        if (!((ps.bm[f][bit >> 5] >> (bit & 31)) & 1u))
+            atomicOr(ps.neg + f * ps.neg_stride + (key >> 5), 1u << (key & 31));
+}
+
 struct PartGeom {
     uint32_t G;        // partition workgroups
     uint32_t cap;      // region capacity in entries (multiple of 32)
@@ -165,7 +184,7 @@ __global__ void __launch_bounds__(kPartThreads) k_part(KeySet ks, uint64_t n, in
                                                        uint32_t* __restrict__ regions, uint32_t* __restrict__ fill,
                                                        uint32_t* __restrict__ subcnt, uint32_t* __restrict__ ovf,
                                                        uint32_t* __restrict__ ovf_count,
-                                                       const uint32_t* __restrict__ bitmap, uint32_t* __restrict__ neg) {
+                                                       ProbeSet ps) {
     constexpr int KPT = part_kpt(KMAX, KM, PROBE);
     extern __shared__ uint32_t smem[];
     const uint32_t B = tm.nbuckets;
@@ -270,11 +289,7 @@ __global__ void __launch_bounds__(kPartThreads) k_part(KeySet ks, uint64_t n, in
                     if (r < pg.cap) {
                         regions[(uint64_t(g) * B + b[u]) * pg.cap + r] = v[u];
                     } else if constexpr (PROBE) {
-                        const uint64_t bit = pos_to_bit((b[u] << tm.tb) | (v[u] & lmask), tm);
-                        if (!((bitmap[bit >> 5] >> (bit & 31)) & 1u)) {
-                            const uint64_t key = s0 + (v[u] >> kSlotShift);
-                            atomicOr(neg + (key >> 5), 1u << (key & 31));
-                        }
+                        spill_probe(ps, pos_to_bit((b[u] << tm.tb) | (v[u] & lmask), tm), s0 + (v[u] >> kSlotShift));
                     } else {
                         ovf[atomicAdd(ovf_count, 1u)] = v[u];
                     }

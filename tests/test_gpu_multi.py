@@ -1,0 +1,134 @@
+"""Multi-filter probe (pbf_probe_multi): one key batch against several SSTable filters, the
+batched form of LsmStorage.get's filter checks (src/lsm_storage.py:164-175; SURVEY.md §8 a-14,
+config C5).  Every hit mask must equal the filter's own single probe and the oracle's."""
+import numpy as np
+import pytest
+
+from pebbledb_amd import BloomFilter, PackedKeys, may_contain_multi, probe_multi_device
+from pebbledb_amd import _native
+from pebbledb_amd._native import PBF_PROBE_DIRECT, PBF_PROBE_TILED
+from pebbledb_amd.keys import splitmix_hex_keys, varlen_keys
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+SEED = 0x5EEDB100
+
+
+def _filters(oracle, nb, k, n_per, count, mode=None, seed=SEED):
+    fs, want = [], []
+    for f in range(count):
+        pk = PackedKeys.fixed(splitmix_hex_keys(seed, f * n_per, n_per))
+        bf = BloomFilter(nb, k)
+        bf.add_many(pk)
+        if mode is not None:
+            bf.set_probe_mode(mode)
+        fs.append(bf)
+        want.append(oracle.build(nb, k, pk))
+    return fs, want
+
+
+@pytest.mark.parametrize("mode", [PBF_PROBE_TILED, PBF_PROBE_DIRECT, None])
+def test_multi_same_size_matches_oracle(oracle, mode):
+    nb, k, n_per, count = 2 ** 20, 6, 40000, 5
+    fs, want = _filters(oracle, nb, k, n_per, count, mode)
+    q = PackedKeys.fixed(splitmix_hex_keys(SEED, n_per // 2, count * n_per))  # members of all + absent
+    got = may_contain_multi(fs, q)
+    for i in range(count):
+        assert np.array_equal(got[i], oracle.probe(want[i], k, q)), i
+        assert np.array_equal(got[i], fs[i].may_contain_many(q, packed=True)), i
+    if mode == PBF_PROBE_TILED:
+        assert all(bf.last_probe_mode == PBF_PROBE_TILED for bf in fs)
+
+
+def test_multi_more_than_eight_filters_and_ragged_n(oracle):
+    nb, k, n_per, count = 2 ** 19, 5, 20000, 11  # two groups of the shared pipeline (8 + 3)
+    fs, want = _filters(oracle, nb, k, n_per, count, PBF_PROBE_TILED)
+    q = PackedKeys.fixed(splitmix_hex_keys(SEED, 3, count * n_per + 13))
+    got = may_contain_multi(fs, q)
+    for i in range(count):
+        assert np.array_equal(got[i], oracle.probe(want[i], k, q)), i
+
+
+def test_multi_mixed_sizes_k0_and_varlen(oracle):
+    """Filters of different (nb_bytes, k), a k = 0 filter (always True) and variable-length keys:
+    the set falls back to per-filter probes with identical results."""
+    d, o = varlen_keys(0xC3, 0, 30000)
+    pk = PackedKeys(d, 30000, offsets=o)
+    shapes = [(2 ** 18, 6), (100003, 7), (2 ** 18, 6), (777, 3)]
+    fs, want = [], []
+    for nb, k in shapes:
+        bf = BloomFilter(nb, k)
+        bf.add_many(pk)
+        fs.append(bf)
+        want.append(oracle.build(nb, k, pk))
+    zero = BloomFilter(64, 0)
+    dq, oq = varlen_keys(0xC3, 15000, 30000)
+    q = PackedKeys(dq, 30000, offsets=oq)
+    got = may_contain_multi(fs + [zero], q)
+    for i, (nb, k) in enumerate(shapes):
+        assert np.array_equal(got[i], oracle.probe(want[i], k, q)), i
+    assert (got[-1][:-1] == 0xFF).all() and got[-1][-1] == 0xFF
+    # same-size subset with variable-length keys takes the shared pipeline
+    fs[0].set_probe_mode(PBF_PROBE_TILED)
+    fs[2].set_probe_mode(PBF_PROBE_TILED)
+    got2 = may_contain_multi([fs[0], fs[2]], q)
+    assert np.array_equal(got2[0], got[0]) and np.array_equal(got2[1], got[2])
+
+
+def test_multi_rejects_bad_sets():
+    a = BloomFilter(4096, 3)
+    a.add("x")
+    with pytest.raises(ValueError):
+        may_contain_multi([a, a], ["x", "y"])
+    b = BloomFilter(0, 3)
+    with pytest.raises(ZeroDivisionError):
+        may_contain_multi([a, b], ["x"])
+
+
+def _dev_hex(seed, start, n, out=None, at=0):
+    t = out if out is not None else torch.empty(n * 16, dtype=torch.uint8, device="cuda")
+    _native.check(_native.lib().pbf_gen_splitmix_hex(0, None, t.data_ptr() + at * 16, seed, start, n), "gen")
+    return t
+
+
+def test_multi_device_c5_shape(oracle):
+    """C5 at reduced size: 8 filters (m = 2^27, k = 6) over disjoint 1M-key SSTables, probed with
+    8M keys (half members spread evenly over the 8 sets, half absent) in one device call; each
+    hit mask equals that filter's single device probe; members all hit; the oracle agrees on
+    every filter for a 200k-key sample."""
+    nf, nb, k, n_per = 8, 2 ** 24, 6, 1_000_000
+    keys = _dev_hex(SEED, 0, nf * n_per)
+    fs = []
+    for f in range(nf):
+        bf = BloomFilter(nb, k)
+        bf.add_device_fixed(keys.data_ptr() + f * n_per * 16, 16, n_per)
+        bf.set_probe_mode(PBF_PROBE_TILED)
+        fs.append(bf)
+    for bf in fs:
+        bf.sync()
+    nq = 8 * n_per
+    half = nq // 2
+    q = torch.empty(nq * 16, dtype=torch.uint8, device="cuda")
+    for f in range(nf):  # members: the first half of each filter's key range
+        _dev_hex(SEED, f * n_per, half // nf, q, f * (half // nf))
+    _dev_hex(SEED, nf * n_per, half, q, half)  # absent
+    hms = [torch.zeros(nq // 8, dtype=torch.uint8, device="cuda") for _ in range(nf)]
+    torch.cuda.synchronize()
+    probe_multi_device(fs, q.data_ptr(), nq, [h.data_ptr() for h in hms], key_len=16)
+    fs[0].sync()
+    assert all(bf.last_probe_mode == PBF_PROBE_TILED for bf in fs)
+    single = torch.zeros(nq // 8, dtype=torch.uint8, device="cuda")
+    qh = q[: 200_000 * 16].cpu().numpy().reshape(-1, 16)
+    per = half // nf
+    for f, bf in enumerate(fs):
+        single.zero_()
+        torch.cuda.synchronize()
+        bf.probe_device_fixed(q.data_ptr(), 16, nq, single.data_ptr())
+        bf.sync()
+        h = hms[f].cpu().numpy()
+        assert np.array_equal(h, single.cpu().numpy()), f
+        bits = np.unpackbits(h, bitorder="little")
+        assert bits[f * per:(f + 1) * per].all(), f  # its own members
+        want = oracle.build(nb, k, PackedKeys.fixed(splitmix_hex_keys(SEED, f * n_per, n_per)), omp=True)
+        assert np.array_equal(h[:25_000], oracle.probe(want, k, PackedKeys.fixed(qh), omp=True)), f

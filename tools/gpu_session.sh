@@ -19,6 +19,7 @@ run() {  # name seconds cmd...
 for step in "$@"; do
   case $step in
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    pytest_multi) run pytest_multi 600 python -u -m pytest tests/test_gpu_multi.py -m gpu -x -v -rf --timeout 300 --timeout-method thread ;;
     pytest) run pytest 900 python -u -m pytest tests -m gpu -x -v -rf --timeout 120 --timeout-method thread ;;
     bench) run bench 600 python bench.py --steps 20 --warmup 5 ;;
     bench_atomic) run bench_atomic 600 python bench.py --steps 10 --warmup 3 --build-mode 1 --no-cpu-baseline ;;
