@@ -42,7 +42,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS) + ["c4", "c5"])
+    ap.add_argument("--c4-keys", type=int, default=125_000_000, help="c4: keys per filter (reference 125M)")
+    ap.add_argument("--c5-probes", type=int, default=100_000_000, help="c5: probe keys (reference 100M)")
     ap.add_argument("--build-mode", type=int, default=0, help="0 auto, 1 atomic, 2 tiled")
     ap.add_argument("--probe-mode", type=int, default=0, help="0 auto, 1 direct, 2 tiled")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -172,6 +174,180 @@ def host_inclusive(bf, keys, n, nb_bytes, L, torch, np, reps=3):
     }
 
 
+def sets_main(args, rank, world, local, torch, dist, np):
+    """Configs 4 and 5: eight independent SSTable filters spread over the ranks (8/N each,
+    shard.filters_for_rank), no collective on the data path.
+
+    c4 — BASELINE.json configs[3]: 1B 16-B keys, filter g built from keys [g*125M, (g+1)*125M)
+         with pebbledb's product sizing (sstable.py:274, fp_rate 0.001 → nb_bytes 224,649,806,
+         k = 10, a non-power-of-two m).  A step = clear + build of every filter the rank owns.
+         value = keys built per step over all ranks / step time (strong scaling: 1B keys total).
+    c5 — configs[4]: filters as C2 (m = 2^30, k = 6, 10M keys each, built before timing); 100M
+         probe keys (half members, 1/8 from each filter's range; half absent) replicated to every
+         rank.  A step = one multi-filter probe (pbf_probe_multi) of the batch against the
+         rank's filters.  value = key x filter probes per step over all ranks / step time."""
+    from math import ceil, log
+
+    from pebbledb_amd import BloomFilter, _native, probe_multi_device
+    from pebbledb_amd.bloom_filter import set_default_device
+    from pebbledb_amd.shard import filters_for_rank
+
+    set_default_device(local)
+    L = _native.lib()
+    mine = filters_for_rank(8, world, rank)
+    if args.config == "c4":
+        n = args.c4_keys
+        p = 0.001
+        m = (-n * log(p)) / (log(2) ** 2)  # bloom_filter.py:109-114, same expression order
+        nb_bytes, k = ceil(m / 8), round((m / n) * log(2))
+        keys = {}
+        for g in mine:
+            keys[g] = torch.empty(n * 16, dtype=torch.uint8, device="cuda")
+            _native.check(L.pbf_gen_splitmix_hex(local, None, keys[g].data_ptr(), SEED, g * n, n), "gen")
+        filters = {g: BloomFilter(nb_bytes, k, device=local) for g in mine}
+        s0 = filters[mine[0]]
+        stream = torch.cuda.ExternalStream(s0.stream)
+        torch.cuda.synchronize()
+
+        def step(ev=None):
+            for i, g in enumerate(mine):
+                bf = filters[g]
+                if ev is not None:
+                    ev[i][0].record(torch.cuda.ExternalStream(bf.stream))
+                bf.clear()
+                bf.add_device_fixed(keys[g].data_ptr(), 16, n)
+                if ev is not None:
+                    ev[i][1].record(torch.cuda.ExternalStream(bf.stream))
+        unit_total = n * 8  # every rank builds its share of the 8 filters per step
+    else:
+        n_f = 10_000_000
+        nb_bytes, k = 2 ** 27, 6
+        nq = args.c5_probes
+        filters = {}
+        kb = torch.empty(n_f * 16, dtype=torch.uint8, device="cuda")
+        for g in mine:
+            _native.check(L.pbf_gen_splitmix_hex(local, None, kb.data_ptr(), SEED, g * n_f, n_f), "gen")
+            torch.cuda.synchronize()
+            bf = BloomFilter(nb_bytes, k, device=local)
+            bf.add_device_fixed(kb.data_ptr(), 16, n_f)
+            bf.sync()
+            filters[g] = bf
+        del kb
+        q = torch.empty(nq * 16, dtype=torch.uint8, device="cuda")
+        half = nq // 2
+        per = half // 8
+        for g in range(8):  # members: 1/8 of the half from each filter's range
+            cnt = per if g < 7 else half - 7 * per
+            _native.check(L.pbf_gen_splitmix_hex(local, None, q.data_ptr() + g * per * 16, SEED, g * n_f, cnt), "gen")
+        _native.check(L.pbf_gen_splitmix_hex(local, None, q.data_ptr() + half * 16, SEED, 8 * n_f, nq - half), "gen")
+        hms = {g: torch.zeros((nq + 7) // 8, dtype=torch.uint8, device="cuda") for g in mine}
+        fl = [filters[g] for g in mine]
+        s0 = fl[0]
+        stream = torch.cuda.ExternalStream(s0.stream)
+        torch.cuda.synchronize()
+
+        def step(ev=None):
+            if ev is not None:
+                ev[0][0].record(stream)
+            probe_multi_device(fl, q.data_ptr(), nq, [hms[g].data_ptr() for g in mine], key_len=16)
+            if ev is not None:
+                ev[0][1].record(stream)
+        unit_total = nq * 8  # key x filter probes per step over all ranks
+
+    nev = len(mine) if args.config == "c4" else 1
+    events = [[[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(nev)] for _ in range(args.steps)]
+    for _ in range(args.warmup):
+        step()
+    for bf in filters.values():
+        bf.sync()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for st in range(args.steps):
+        step(events[st])
+    for bf in filters.values():
+        bf.sync()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    pass_ms = sum(e[i][0].elapsed_time(e[i][1]) for e in events for i in range(nev)) / (args.steps * nev)
+    # correctness on the measured state
+    ok = True
+    fp_rate = None
+    if args.config == "c4":
+        g = mine[0]
+        bf = filters[g]
+        hm = torch.zeros((n + 7) // 8, dtype=torch.uint8, device="cuda")
+        bf.probe_device_fixed(keys[g].data_ptr(), 16, n, hm.data_ptr())
+        bf.sync()
+        ok = bool((np.unpackbits(hm.cpu().numpy(), bitorder="little")[:n] == 1).all())
+        absent = torch.empty(1_000_000 * 16, dtype=torch.uint8, device="cuda")
+        _native.check(L.pbf_gen_splitmix_hex(local, None, absent.data_ptr(), SEED, 8 * n, 1_000_000), "gen")
+        hm2 = torch.zeros(125_000, dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()
+        bf.probe_device_fixed(absent.data_ptr(), 16, 1_000_000, hm2.data_ptr())
+        bf.sync()
+        fp_rate = float(np.unpackbits(hm2.cpu().numpy()).sum()) / 1e6
+    else:
+        for g in mine:
+            bits = np.unpackbits(hms[g].cpu().numpy(), bitorder="little")
+            cnt = per if g < 7 else half - 7 * per
+            ok &= bool(bits[g * per:g * per + cnt].all())
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        okt = torch.tensor([1 if ok else 0], dtype=torch.int32, device="cuda")
+        dist.all_reduce(okt, op=dist.ReduceOp.MIN)
+        ok = bool(okt.item())
+    if rank == 0:
+        ms = elapsed / args.steps * 1e3
+        if args.config == "c4":
+            b_pass = algorithmic_bytes(n, 16.0, k, 8 * nb_bytes, False)
+            metric, unit = "Mkeys/s bloom build, 1B 16B keys into 8 product-sized SSTable filters", "Mkeys/s"
+            what = (f"c4: 8 filters x {n} 16-B keys (product sizing fp 0.001: nb_bytes={nb_bytes}, k={k}); "
+                    f"a step builds every filter once; filters {len(mine)}/rank")
+            pk = "build pass of the rank's filters (clear + tiled build each, concurrent streams)"
+        else:
+            b_pass = probe_bytes(nq, 16.0, k, False) * len(mine)
+            metric, unit = "Mprobes/s (key x filter) batched probe, 100M keys vs 8x128MiB filters", "Mprobes/s"
+            what = (f"c5: {nq} probe keys (half members) x 8 filters (nb_bytes=2^27, k=6, 10M keys each); "
+                    f"a step = one pbf_probe_multi over the rank's {len(mine)} filters")
+            pk = "multi-filter probe (shared k_part + per-filter k_tile_probe/k_gather)"
+        if args.config == "c4":
+            # the rank's filters build concurrently on their own streams, so per-filter event
+            # spans overlap: the pass rate is all of the rank's filters' bytes per step time
+            b_pass *= len(mine)
+            pass_ms = ms
+        ach = b_pass / (pass_ms * 1e-3) / 1e9
+        out = {
+            "metric": metric, "value": round(unit_total / (ms * 1e-3) / 1e6, 3),
+            "unit": unit, "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 4),
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u32",
+            "data": "synthetic (splitmix64 hex keys generated on device)",
+            "config": {"workload": what, "nb_bytes": nb_bytes, "k": k, "filters_per_rank": len(mine),
+                       "parallelism": f"filters-over-gpus x{world}"},
+            "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "kernel": pk,
+                         "algorithmic_bytes": int(b_pass), "avg_ms": round(pass_ms, 4)},
+            "check": {"members_all_hit": ok},
+        }
+        if fp_rate is not None:
+            out["check"]["fp_rate_1M_absent"] = fp_rate
+        if args.config == "c5":
+            # the same work as independent single-filter probes (no shared partition)
+            tq = []
+            for _ in range(2):
+                t1 = time.perf_counter()
+                for g in mine:
+                    filters[g].probe_device_fixed(q.data_ptr(), 16, nq, hms[g].data_ptr())
+                for g in mine:
+                    filters[g].sync()
+                tq.append(time.perf_counter() - t1)
+            out["per_filter_probes_ms"] = round(min(tq) * 1e3, 3)
+        print(json.dumps(out), flush=True)
+
+
 def main():
     args = parse()
     rank = int(os.environ.get("RANK", "0"))
@@ -187,6 +363,12 @@ def main():
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group(backend="nccl", init_method="env://", device_id=torch.device("cuda", local))
+
+    if args.config in ("c4", "c5"):
+        sets_main(args, rank, world, local, torch, dist, np)
+        if world > 1:
+            dist.destroy_process_group()
+        return
 
     from pebbledb_amd import BloomFilter, _native
     from pebbledb_amd.bloom_filter import set_default_device

@@ -305,7 +305,7 @@ uint32_t ring_entries(uint32_t B, uint32_t k, bool probe, uint32_t tb) {
     return uint64_t(kRingKeysPerSub) * k * 4 <= uint64_t(B) * rc ? rc : 0;
 }
 
-PartPlan plan_ring(uint32_t B, uint32_t k, uint64_t n, uint32_t rc) {
+PartPlan plan_ring(uint32_t B, uint32_t k, uint64_t n, uint32_t rc, double share) {
     PartPlan pl{};
     const uint64_t kps = kRingKeysPerSub;
     const uint64_t G0 = std::min<uint64_t>(256, std::max<uint64_t>(1, (n + kps - 1) / kps));
@@ -317,7 +317,7 @@ PartPlan plan_ring(uint32_t B, uint32_t k, uint64_t n, uint32_t rc) {
     pl.pg.nsub = uint32_t(kpw / kps);
     pl.pg.nq = (pl.pg.nsub + 3) / 4;
     pl.pg.ring = rc;
-    const double mu = double(kpw) * k / B;
+    const double mu = double(kpw) * k * share;
     const uint64_t cap = uint64_t(mu + 8.0 * std::sqrt(mu) + 32.0);
     pl.pg.cap = uint32_t(((cap + 31) / 32) * 32);
     pl.lds_part = size_t((2 * B + 16 * 128 + 3) & ~3u) * 4 + size_t(B) * rc * 4;
@@ -325,7 +325,7 @@ PartPlan plan_ring(uint32_t B, uint32_t k, uint64_t n, uint32_t rc) {
     return pl;
 }
 
-PartPlan plan_partition(uint32_t B, uint32_t k, int km, uint64_t n, bool probe) {
+PartPlan plan_partition(uint32_t B, uint32_t k, int km, uint64_t n, bool probe, double share) {
     PartPlan pl{};
     const size_t per_entry = probe ? 6 : 4;  // stage u32 (+ u16 tile id for probes)
     const size_t fixed = size_t(3 * B + 1 + 16) * 4;
@@ -342,27 +342,50 @@ PartPlan plan_partition(uint32_t B, uint32_t k, int km, uint64_t n, bool probe) 
     pl.pg.kps = uint32_t(kps);
     pl.pg.kpw = kpw;
     pl.pg.nsub = uint32_t(kpw / kps);
-    const double mu = double(kpw) * k / B;
+    const double mu = double(kpw) * k * share;
     const uint64_t cap = uint64_t(mu + 8.0 * std::sqrt(mu) + 32.0);
     pl.pg.cap = uint32_t(((cap + 31) / 32) * 32);
     pl.lds_gather = size_t((pl.pg.kpw + 31) / 32) * 4 + size_t(B) * (pl.pg.nsub + 1) * 2 + 16;
     return pl;
 }
 
-PartPlan plan_for(uint32_t B, uint32_t k, int km, uint64_t n, bool probe, uint32_t tb) {
-    const uint32_t rc = ring_entries(B, k, probe, tb);
+// Expected share of one hash in the busiest tile.  The reference's floor-mod of a signed 32-bit
+// hash (bloom_filter.py:47) is uniform only for power-of-two m: for m < 2^31 a position has
+// 2*floor(2^31/m) or 2*ceil(2^31/m) preimages (the first and last 2^31 mod m positions get the
+// extra ones), for 2^31 <= m < 2^32 the overlap [m - 2^31, 2^31) gets 2; above 2^32 the tile
+// space is the 2^32 reachable positions, one preimage each.  Region capacity is sized for the
+// densest tile so edge tiles of a non-power-of-two filter do not overflow.
+double busiest_tile_share(const TileMap& tm) {
+    const double tile = double(uint64_t(1) << tm.tb);
+    const uint64_t m = tm.im.m;
+    double max_pre;
+    if (tm.cspace)
+        max_pre = 1.0;
+    else if (tm.im.mode == kPow2)
+        max_pre = 4294967296.0 / double(m);
+    else if (m < (uint64_t(1) << 31))
+        max_pre = 2.0 * double(((uint64_t(1) << 31) + m - 1) / m);
+    else
+        max_pre = 2.0;
+    return std::min(1.0, max_pre * tile / 4294967296.0);
+}
+
+PartPlan plan_for(const TileMap& tm, uint32_t k, int km, uint64_t n, bool probe) {
+    const uint32_t B = tm.nbuckets;
+    const double share = busiest_tile_share(tm);
+    const uint32_t rc = ring_entries(B, k, probe, tm.tb);
     if (rc) {
-        const PartPlan pl = plan_ring(B, k, n, rc);
+        const PartPlan pl = plan_ring(B, k, n, rc, share);
         if (pl.pg.cap < (1u << 20)) return pl;  // flush descriptors hold a region position in 20 bits
     }
-    return plan_partition(B, k, km, n, probe);
+    return plan_partition(B, k, km, n, probe, share);
 }
 
 int run_tiled(pbf_filter_t* f, const Batch& b) {
     const TileMap& tm = f->tm;
     const uint32_t B = tm.nbuckets;
     const uint32_t k = f->k;
-    const PartPlan pl = plan_for(B, k, b.km, b.n, false, tm.tb);
+    const PartPlan pl = plan_for(tm, k, b.km, b.n, false);
     const PartGeom& pg = pl.pg;
     HIP_TRY(f->regions.ensure(size_t(pg.G) * B * pg.cap * 4));
     HIP_TRY(f->fill.ensure(size_t(pg.G) * B * 4));
@@ -408,15 +431,15 @@ int run_tiled(pbf_filter_t* f, const Batch& b) {
 }
 
 // Tiled probe of one key batch against nf filters sharing (m, k) (nf = 1: a plain probe).  The
-// keys are hashed and partitioned once, on fs[0]'s stream with fs[0]'s scratch; the tile test
-// and the gather then run once per filter.  hitmasks[i] + hm_off is filter i's output.
-int run_tiled_probe_set(pbf_filter_t* const* fs, uint32_t nf, const Batch& b, uint8_t* const* hitmasks,
-                        uint64_t hm_off) {
-    pbf_filter_t* f = fs[0];
+// keys are hashed and partitioned once, on f's stream with f's scratch (f = the set's first
+// filter, also for every later group of a large set); the tile test and the gather then run
+// once per filter.  hitmasks[i] + hm_off is filter i's output.
+int run_tiled_probe_set(pbf_filter_t* f, pbf_filter_t* const* fs, uint32_t nf, const Batch& b,
+                        uint8_t* const* hitmasks, uint64_t hm_off) {
     const TileMap& tm = f->tm;
     const uint32_t B = tm.nbuckets;
     const uint32_t k = f->k;
-    const PartPlan pl = plan_for(B, k, b.km, b.n, true, tm.tb);
+    const PartPlan pl = plan_for(tm, k, b.km, b.n, true);
     const PartGeom& pg = pl.pg;
     HIP_TRY(f->regions.ensure(size_t(pg.G) * B * pg.cap * 4));
     HIP_TRY(f->fill.ensure(size_t(pg.G) * B * 4));
@@ -500,7 +523,7 @@ int run_tiled_probe_set(pbf_filter_t* const* fs, uint32_t nf, const Batch& b, ui
 int run_tiled_probe(pbf_filter_t* f, const Batch& b, uint8_t* hitmask) {
     pbf_filter_t* fs[1] = {f};
     uint8_t* outs[1] = {hitmask};
-    return run_tiled_probe_set(fs, 1, b, outs, 0);
+    return run_tiled_probe_set(f, fs, 1, b, outs, 0);
 }
 
 // The partition pass needs its tile counters plus a stage of one key per thread in LDS.
@@ -533,10 +556,10 @@ bool want_tiled_probe(pbf_filter_t* f, uint64_t n) {
 // Largest probe batch one tiled pipeline takes: k_gather keeps a u16 run-boundary table
 // (B x (nsub+1)) and a bit per key of its workgroup in LDS, and positions stay u32.
 uint64_t tiled_probe_batch(pbf_filter_t* f, int km) {
-    const uint32_t B = f->tm.nbuckets, k = f->k;
+    const uint32_t k = f->k;
     uint64_t n = std::max<uint64_t>(64, (kMaxPositions / k) & ~uint64_t(63));
     for (;;) {
-        const PartPlan pl = plan_for(B, k, km, n, true, f->tm.tb);
+        const PartPlan pl = plan_for(f->tm, k, km, n, true);
         if ((pl.lds_gather <= 156 * 1024 && pl.pg.cap <= 65535) || n <= 64 * 1024) return n;
         n = std::max<uint64_t>(64 * 1024, (n / 2) & ~uint64_t(63));
     }
@@ -641,7 +664,8 @@ int probe_multi_device(pbf_filter_t* const* fs, uint32_t nf, const Batch& b, uin
             else
                 c.ks.data = b.ks.data + i0 * b.ks.key_len;
             for (uint32_t g0 = 0; g0 < nf; g0 += kMaxProbeSet) {
-                rc = run_tiled_probe_set(fs + g0, std::min<uint32_t>(kMaxProbeSet, nf - g0), c, hitmasks + g0, i0 / 8);
+                rc = run_tiled_probe_set(f0, fs + g0, std::min<uint32_t>(kMaxProbeSet, nf - g0), c, hitmasks + g0,
+                                         i0 / 8);
                 if (rc) return rc;
             }
         }

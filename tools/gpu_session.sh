@@ -22,6 +22,13 @@ for step in "$@"; do
     pytest_multi) run pytest_multi 600 python -u -m pytest tests/test_gpu_multi.py -m gpu -x -v -rf --timeout 300 --timeout-method thread ;;
     pytest) run pytest 900 python -u -m pytest tests -m gpu -x -v -rf --timeout 120 --timeout-method thread ;;
     bench) run bench 600 python bench.py --steps 20 --warmup 5 ;;
+    bench_c3) run bench_c3 600 python bench.py --config c3 --steps 5 --warmup 2 --no-cpu-baseline ;;
+    bench_c4) run bench_c4 600 python bench.py --config c4 --steps 3 --warmup 1 ;;
+    bench_c5) run bench_c5 600 python bench.py --config c5 --steps 5 --warmup 2 ;;
+    prof_c34) run prof_c4 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_c4 -o run -- python bench.py --config c4 --steps 2 --warmup 1
+              python tools/prof_summary.py gpurun_out/prof_c4 > gpurun_out/prof_c4_summary.txt 2>&1
+              run prof_c3 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_c3 -o run -- python bench.py --config c3 --steps 3 --warmup 1 --no-cpu-baseline
+              python tools/prof_summary.py gpurun_out/prof_c3 > gpurun_out/prof_c3_summary.txt 2>&1 ;;
     bench_atomic) run bench_atomic 600 python bench.py --steps 10 --warmup 3 --build-mode 1 --no-cpu-baseline ;;
     bench_tt) run bench_tt 300 python bench.py --steps 20 --warmup 5 --build-mode 2 --probe-mode 2 --no-cpu-baseline --no-host-inclusive ;;
     bench_modes) for bm in 1 2; do for pm in 1 2; do run bench_b${bm}_p${pm} 300 python bench.py --steps 20 --warmup 5 --build-mode $bm --probe-mode $pm --no-cpu-baseline; done; done ;;
