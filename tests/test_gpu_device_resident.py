@@ -108,3 +108,62 @@ def test_config2_full_size_properties(oracle):
     # the non-member hit mask equals the oracle's on a 1M sample
     qs = PackedKeys.fixed(splitmix_hex_keys(0x5EEDB100, n, 1_000_000))
     assert np.array_equal(h[n // 8: n // 8 + 125000], oracle.probe(want, k, qs, omp=True))
+
+
+@pytest.mark.timeout(300)
+def test_config4_full_size_product_sizing(oracle):
+    """C4: one of the eight 125M-key SSTable filters with pebbledb's product sizing
+    (sstable.py:274, fp 0.001 → nb_bytes 224,649,806, k = 10: non-power-of-two m, the
+    Lemire-fastmod floor-mod path).  Tiled build == the C oracle bit for bit; members all hit."""
+    from math import ceil, log
+    n = 125_000_000
+    m = (-n * log(0.001)) / (log(2) ** 2)
+    nb, k = ceil(m / 8), round((m / n) * log(2))
+    assert (nb, k) == (224_649_806, 10)
+    keys = dev_keys_hex(0x5EEDB100, 3 * n, n)  # filter 3's key range
+    bf = BloomFilter(nb, k)
+    bf.set_build_mode(PBF_BUILD_TILED)
+    bf.add_device_fixed(keys.data_ptr(), 16, n)
+    hm = torch.zeros(n // 8, dtype=torch.uint8, device="cuda")
+    bf.probe_device_fixed(keys.data_ptr(), 16, n, hm.data_ptr())
+    bf.sync()
+    assert bf.last_build_mode == PBF_BUILD_TILED
+    assert bool((hm == 0xFF).all().item())
+    got = bf.bitmap()
+    host = PackedKeys.fixed(keys.cpu().numpy().reshape(-1, 16))
+    del keys, hm
+    want = oracle.build(nb, k, host, omp=True)
+    assert got == want.tobytes()
+
+
+@pytest.mark.timeout(300)
+def test_config3_full_size_varlen_large_m(oracle):
+    """C3: 100M variable-length keys (8..64 B) into m = 2^33 bits (nb_bytes = 2^30), k = 8 — the
+    m > 2^32 index map where only [0, 2^31) and [m - 2^31, m) are reachable.  Tiled build ==
+    the C oracle bit for bit; members all hit; the unreachable middle stays zero."""
+    from pebbledb_amd.keys import _splitmix64_np
+    n, nb, k = 100_000_000, 2 ** 30, 8
+    idx = np.arange(n, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        h = _splitmix64_np((np.uint64(0xC3) << np.uint64(32)) + idx)
+    o = np.zeros(n + 1, dtype=np.uint64)
+    np.cumsum((np.uint64(8) + h % np.uint64(57)), out=o[1:])
+    del h, idx
+    od = torch.from_numpy(o.view(np.int64)).cuda()
+    d = torch.empty(int(o[-1]), dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    _native.check(_native.lib().pbf_gen_varlen(0, None, d.data_ptr(), od.data_ptr(), 0xC3, 0, n), "gen")
+    torch.cuda.synchronize()
+    bf = BloomFilter(nb, k)
+    bf.set_build_mode(PBF_BUILD_TILED)
+    bf.add_device(d.data_ptr(), od.data_ptr(), n)
+    hm = torch.zeros(n // 8, dtype=torch.uint8, device="cuda")
+    bf.probe_device(d.data_ptr(), od.data_ptr(), n, hm.data_ptr())
+    bf.sync()
+    assert bool((hm == 0xFF).all().item())
+    got = np.frombuffer(bf.bitmap(), dtype=np.uint8)
+    assert not got[2 ** 28: nb - 2 ** 28].any()  # bits [2^31, m - 2^31) are unreachable
+    host = PackedKeys(d.cpu().numpy(), n, offsets=o)
+    del d, od, hm
+    want = oracle.build(nb, k, host, omp=True)
+    assert np.array_equal(got, want)
