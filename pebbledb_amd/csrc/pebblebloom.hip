@@ -119,6 +119,17 @@ int probe_stage1() {
     return v;
 }
 
+// Tile-range splits of the ring probe's gather (PBF_GATHER_SPLIT overrides; 1 = one workgroup
+// per partition workgroup, writing the hit mask directly).
+uint32_t gather_splits() {
+    static const uint32_t v = [] {
+        const char* e = std::getenv("PBF_GATHER_SPLIT");
+        const int x = e ? std::atoi(e) : 0;
+        return x > 0 ? uint32_t(std::min(x, 64)) : 8u;
+    }();
+    return v;
+}
+
 int kmax_for(uint32_t k) {
     if (k <= 4) return 4;
     if (k <= 8) return 8;
@@ -206,7 +217,7 @@ struct pbf_filter {
     bool tiled_ok = false;
     int probe_mode = PBF_PROBE_AUTO;
     int last_probe_mode = 0;
-    DevBuf regions, fill, ovf, ovf_count, subcnt, rbits, neg, alive;
+    DevBuf regions, fill, ovf, ovf_count, subcnt, rbits, neg, alive, hw;
     DevBuf dkeys, doffs, dout;
     PinBuf pin[2];
     int pin_next = 0;
@@ -455,6 +466,15 @@ int run_tiled_probe_set(pbf_filter_t* f, pbf_filter_t* const* fs, uint32_t nf, c
     auto* R = static_cast<uint32_t*>(f->rbits.p);
     auto* neg = static_cast<uint32_t*>(f->neg.p);
     hipStream_t s = f->stream;
+    // ring gather split over S tile ranges (several small workgroups per CU)
+    const uint32_t S = pg.ring ? gather_splits() : 1;
+    const size_t lds_gather_split =
+        pg.ring ? size_t((pg.kpw + 31) / 32) * 4 + size_t((B + S - 1) / S) * (pg.nq + 1) * 2 + 16 : pl.lds_gather;
+    uint32_t* hw = nullptr;
+    if (S > 1) {
+        HIP_TRY(f->hw.ensure(neg_bytes));
+        hw = static_cast<uint32_t*>(f->hw.p);
+    }
     ProbeSet ps{};
     ps.nf = nf;
     ps.neg = neg;
@@ -492,15 +512,23 @@ int run_tiled_probe_set(pbf_filter_t* f, pbf_filter_t* const* fs, uint32_t nf, c
         });
         HIP_TRY(err);
         CHECK_LAUNCH();
-        if (pg.ring) HIP_TRY(allow_lds(k_gather_ring, pl.lds_gather));
+        if (pg.ring) HIP_TRY(allow_lds(k_gather_ring, lds_gather_split));
         else HIP_TRY(allow_lds(k_gather, pl.lds_gather));
         for (uint32_t i = 0; i < nf; ++i) {
+            if (S > 1) HIP_TRY(hipMemsetAsync(hw, 0xFF, neg_bytes, s));
             k_tile_probe<<<B, 1024, lds_tile, s>>>(tm, pg, regions, fill, fs[i]->bitmap, R, expand);
             CHECK_LAUNCH();
             const uint32_t* negi = neg + i * neg_words;
             if (pg.ring)
-                k_gather_ring<<<pg.G, 1024, pl.lds_gather, s>>>(tm, pg, b.n, regions, R, fill, subcnt, negi, alive,
-                                                               outs[i] + hm_off);
+            {
+                const dim3 grid(pg.G, S);
+                k_gather_ring<<<grid, 512, lds_gather_split, s>>>(tm, pg, b.n, regions, R, fill, subcnt, negi, alive,
+                                                                 outs[i] + hm_off, hw);
+                if (S > 1) {
+                    CHECK_LAUNCH();
+                    k_hw_to_hitmask<<<grid_for(neg_words, 256, 4096), 256, 0, s>>>(hw, b.n, outs[i] + hm_off);
+                }
+            }
             else
                 k_gather<<<pg.G, 1024, pl.lds_gather, s>>>(tm, pg, b.n, regions, R, subcnt, negi, outs[i] + hm_off);
             CHECK_LAUNCH();
@@ -958,7 +986,7 @@ int pbf_destroy(pbf_filter_t* f) {
     if (f->stream) (void)hipStreamSynchronize(f->stream);
     if (f->bitmap) (void)hipFree(f->bitmap);
     if (f->dpop) (void)hipFree(f->dpop);
-    for (DevBuf* d : {&f->regions, &f->fill, &f->ovf, &f->ovf_count, &f->subcnt, &f->rbits, &f->neg, &f->alive})
+    for (DevBuf* d : {&f->regions, &f->fill, &f->ovf, &f->ovf_count, &f->subcnt, &f->rbits, &f->neg, &f->alive, &f->hw})
         d->release();
     f->dkeys.release();
     f->doffs.release();

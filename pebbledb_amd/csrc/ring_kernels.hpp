@@ -241,31 +241,41 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
     }
 }
 
-// Probe gather for the ring partition: workgroup g owns keys [g*kpw, (g+1)*kpw) and regions
-// (g, 0..B-1).  Entries of sub-chunks 4q..4q+3 lie in [pref[q], pref[q+1]) of their region, so a
-// failed entry at position r belongs to sub-chunk 4q + (entry >> 30) with q the last group whose
+// Probe gather for the ring partition: workgroup (g, sp) owns the keys [g*kpw, (g+1)*kpw) of
+// partition workgroup g and the tiles [sp*B/S, (sp+1)*B/S) of its regions (S = gridDim.y
+// splits, so the gather runs several small workgroups per CU instead of one large one).
+// Entries of sub-chunks 4q..4q+3 lie in [pref[q], pref[q+1]) of their region, so a failed entry
+// at position r belongs to sub-chunk 4q + (entry >> 30) with q the last group whose
 // pref[q] <= r; its key is that sub-chunk's first key + the entry's slot.  A failed entry clears
-// its key's bit in an LDS bitmap of the workgroup's keys, written out as hit-mask words.
-//   LDS: kbits[kpw/32], pref rows of the workgroup as u16 (B x (nq+1)).
-__global__ void __launch_bounds__(1024) k_gather_ring(TileMap tm, PartGeom pg, uint64_t n,
-                                                      const uint32_t* __restrict__ regions,
-                                                      const uint32_t* __restrict__ R, const uint32_t* __restrict__ fill,
-                                                      const uint32_t* __restrict__ pref,
-                                                      const uint32_t* __restrict__ neg, const uint32_t* __restrict__ alive,
-                                                      uint8_t* __restrict__ hitmask) {
+// its key's bit in an LDS bitmap of the workgroup's keys.  S = 1 writes the hit-mask words
+// directly; S > 1 ANDs them into `hw` (one u32 per 32 keys, preset to all ones) and
+// k_hw_to_hitmask writes the hit mask.
+//   LDS: kbits[kpw/32], pref rows of the split's tiles as u16 ((B/S) x (nq+1)).
+__global__ void __launch_bounds__(512) k_gather_ring(TileMap tm, PartGeom pg, uint64_t n,
+                                                     const uint32_t* __restrict__ regions,
+                                                     const uint32_t* __restrict__ R, const uint32_t* __restrict__ fill,
+                                                     const uint32_t* __restrict__ pref,
+                                                     const uint32_t* __restrict__ neg, const uint32_t* __restrict__ alive,
+                                                     uint8_t* __restrict__ hitmask, uint32_t* __restrict__ hw) {
     extern __shared__ uint32_t smem[];
     const uint32_t B = tm.nbuckets, cap = pg.cap, wpr = cap / 32, nqs = pg.nq + 1;
     const uint32_t tid = threadIdx.x, nt = blockDim.x;
     const uint32_t lane = tid & 63, wave = tid >> 6, nwaves = nt >> 6;
     const uint32_t g = blockIdx.x;
+    const uint32_t S = gridDim.y, sp = blockIdx.y;
+    const uint32_t b_lo = uint32_t(uint64_t(B) * sp / S), b_hi = uint32_t(uint64_t(B) * (sp + 1) / S);
+    const uint32_t nb = b_hi - b_lo;
     const uint64_t k0 = uint64_t(g) * pg.kpw;
     const uint64_t k1 = min(n, k0 + pg.kpw);
     const uint32_t nkeys = uint32_t(k1 - k0);
     const uint32_t kw = uint32_t((pg.kpw + 31) / 32);
     uint32_t* kbits = smem;                                    // kw words
-    uint16_t* lpref = reinterpret_cast<uint16_t*>(kbits + kw);  // B * nqs (values <= cap < 2^16)
+    uint16_t* lpref = reinterpret_cast<uint16_t*>(kbits + kw);  // nb * nqs (values <= cap < 2^16)
     const uint32_t* gp = pref + uint64_t(g) * nqs * B;  // [q][b] in memory, [b][q] in LDS
-    for (uint32_t x = tid; x < B * nqs; x += nt) lpref[(x % B) * nqs + x / B] = uint16_t(gp[x]);
+    for (uint32_t x = tid; x < nb * nqs; x += nt) {
+        const uint32_t q = x / nb, bb = x - q * nb;
+        lpref[bb * nqs + q] = uint16_t(gp[uint64_t(q) * B + b_lo + bb]);
+    }
     for (uint32_t w = tid; w < kw; w += nt) {
         const uint32_t key0 = w * 32;
         uint32_t m = key0 >= nkeys ? 0u : (nkeys - key0 >= 32 ? ~0u : ((1u << (nkeys - key0)) - 1u));
@@ -277,10 +287,11 @@ __global__ void __launch_bounds__(1024) k_gather_ring(TileMap tm, PartGeom pg, u
     }
     lds_barrier();
     constexpr int U = 4;
-    for (uint32_t b0 = wave; b0 < B; b0 += nwaves * U) {
+    for (uint32_t b0 = b_lo + wave; b0 < b_hi; b0 += nwaves * U) {
         uint32_t fillb[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) fillb[u] = b0 + u * nwaves < B ? fill[uint64_t(b0 + u * nwaves) * pg.G + g] : 0u;
+        for (int u = 0; u < U; ++u)
+            fillb[u] = b0 + u * nwaves < b_hi ? fill[uint64_t(b0 + u * nwaves) * pg.G + g] : 0u;
         uint32_t maxf = 0;
 #pragma unroll
         for (int u = 0; u < U; ++u) maxf = max(maxf, fillb[u]);
@@ -289,7 +300,7 @@ __global__ void __launch_bounds__(1024) k_gather_ring(TileMap tm, PartGeom pg, u
             uint32_t rw[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                const uint32_t b = min(b0 + u * nwaves, B - 1);
+                const uint32_t b = min(b0 + u * nwaves, b_hi - 1);
                 const uint32_t r = min(r0 + lane * 4, (max(fillb[u], 1u) - 1) & ~3u);
                 const uint64_t reg = uint64_t(g) * B + b;
                 v[u] = *reinterpret_cast<const uint4*>(regions + reg * cap + r);
@@ -299,13 +310,13 @@ __global__ void __launch_bounds__(1024) k_gather_ring(TileMap tm, PartGeom pg, u
             for (int u = 0; u < U; ++u) {
                 const uint32_t b = b0 + u * nwaves;
                 const uint32_t r = r0 + lane * 4;
-                if (b < B && r < fillb[u]) {
+                if (b < b_hi && r < fillb[u]) {
                     uint32_t fails = ~r_quad(rw[u], r) & 0xFu;
                     if (fillb[u] - r < 4) fails &= (1u << (fillb[u] - r)) - 1u;
                     if (fails) {
                         // q = the last group with pref[q] <= r (pref non-decreasing, pref[0] = 0);
                         // a fixed-trip binary search keeps the wave's lanes together
-                        const uint16_t* pb = lpref + b * nqs;
+                        const uint16_t* pb = lpref + (b - b_lo) * nqs;
                         uint32_t lo = 0, len = nqs;
                         while (len > 1) {
                             const uint32_t half = len >> 1;
@@ -328,14 +339,32 @@ __global__ void __launch_bounds__(1024) k_gather_ring(TileMap tm, PartGeom pg, u
         }
     }
     lds_barrier();
+    if (S > 1) {
+        for (uint32_t w = tid; w * 32 < nkeys; w += nt) atomicAnd(hw + (k0 >> 5) + w, kbits[w]);
+        return;
+    }
     for (uint32_t w = tid; w * 32 < nkeys; w += nt) {
         const uint64_t key0 = k0 + uint64_t(w) * 32;
         const uint32_t bits = kbits[w];
-        const uint64_t nb = min<uint64_t>(4, (n - key0 + 7) / 8);
-        if (nb == 4 && (reinterpret_cast<uintptr_t>(hitmask + key0 / 8) & 3) == 0)
+        const uint64_t nbt = min<uint64_t>(4, (n - key0 + 7) / 8);
+        if (nbt == 4 && (reinterpret_cast<uintptr_t>(hitmask + key0 / 8) & 3) == 0)
             *reinterpret_cast<uint32_t*>(hitmask + key0 / 8) = bits;
         else
-            for (uint64_t q = 0; q < nb; ++q) hitmask[key0 / 8 + q] = uint8_t(bits >> (8 * q));
+            for (uint64_t q = 0; q < nbt; ++q) hitmask[key0 / 8 + q] = uint8_t(bits >> (8 * q));
+    }
+}
+
+// hw (ANDed gather words, one per 32 keys) → the LSB-first hit mask of n keys.
+__global__ void k_hw_to_hitmask(const uint32_t* __restrict__ hw, uint64_t n, uint8_t* __restrict__ hitmask) {
+    const uint64_t nw = (n + 31) / 32;
+    for (uint64_t w = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; w < nw; w += uint64_t(gridDim.x) * blockDim.x) {
+        const uint64_t key0 = w * 32;
+        const uint32_t bits = hw[w];
+        const uint64_t nbt = min<uint64_t>(4, (n - key0 + 7) / 8);
+        if (nbt == 4 && (reinterpret_cast<uintptr_t>(hitmask + key0 / 8) & 3) == 0)
+            *reinterpret_cast<uint32_t*>(hitmask + key0 / 8) = bits;
+        else
+            for (uint64_t q = 0; q < nbt; ++q) hitmask[key0 / 8 + q] = uint8_t(bits >> (8 * q));
     }
 }
 

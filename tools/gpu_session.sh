@@ -29,6 +29,7 @@ for step in "$@"; do
               python tools/prof_summary.py gpurun_out/prof_c4 > gpurun_out/prof_c4_summary.txt 2>&1
               run prof_c3 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_c3 -o run -- python bench.py --config c3 --steps 3 --warmup 1 --no-cpu-baseline
               python tools/prof_summary.py gpurun_out/prof_c3 > gpurun_out/prof_c3_summary.txt 2>&1 ;;
+    gsplit) for sp in ${PBF_SPLITS:-8 12 16}; do PBF_GATHER_SPLIT=$sp run gsplit_$sp 300 python bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-host-inclusive; done ;;
     bench_atomic) run bench_atomic 600 python bench.py --steps 10 --warmup 3 --build-mode 1 --no-cpu-baseline ;;
     bench_tt) run bench_tt 300 python bench.py --steps 20 --warmup 5 --build-mode 2 --probe-mode 2 --no-cpu-baseline --no-host-inclusive ;;
     bench_modes) for bm in 1 2; do for pm in 1 2; do run bench_b${bm}_p${pm} 300 python bench.py --steps 20 --warmup 5 --build-mode $bm --probe-mode $pm --no-cpu-baseline; done; done ;;
