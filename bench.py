@@ -24,7 +24,7 @@ sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
 # per-pass HBM bytes from rocprofv3 PMC passes of this same bench (tools/traffic_summary.py);
-# used only when it was measured on the very library this run loads (sha256 match)
+# used only when it was measured on the very kernel sources this run was built from
 TRAFFIC_FILE = os.path.join(REPO, "profiles", "traffic_{config}.json")
 
 CONFIGS = {
@@ -65,16 +65,15 @@ def probe_bytes(n, L, k, offsets):
     return n * L + 4 * n * k + n // 8 + (8 * n if offsets else 0)
 
 
-def measured_traffic(config: str, lib_path: str) -> dict | None:
+def measured_traffic(config: str) -> dict | None:
     """{"build": bytes, "probe": bytes, "source": ...} from the committed PMC summary, or None
-    when there is none for this config or it was taken on a different libpebblebloom.so."""
-    import hashlib
+    when there is none for this config or it was taken on other kernel sources."""
+    from pebbledb_amd.build import source_digest
     path = TRAFFIC_FILE.format(config=config)
-    if not os.path.exists(path):
+    if not os.path.exists(path) or os.environ.get("PBF_LIB"):
         return None
     t = json.load(open(path))
-    sha = hashlib.sha256(open(lib_path, "rb").read()).hexdigest()
-    if t.get("lib_sha256") != sha:
+    if t.get("source_sha256") != source_digest():
         return None
     out = {p: v["traffic_bytes"] for p, v in t["passes"].items()}
     out["source"] = os.path.relpath(path, REPO) + ": " + t["source"] + "; " + t["correction"]
@@ -491,7 +490,7 @@ def main():
         else:
             dom = {"kernel": ("probe pass (tiled: k_part<probe>+k_tile_probe+k_gather)" if bf.last_probe_mode == 2
                               else "k_probe"), "achieved": ach_probe, "ms": probe_ms, "bytes": b_probe}
-        traffic = measured_traffic(args.config, _native.lib_path())
+        traffic = measured_traffic(args.config)
         dom_pass = "build" if build_ms >= probe_ms else "probe"
         out = {
             "metric": "Mkeys/s bloom build+probe (device-resident), 10M 16B keys; 1/2/4/8 GPU",

@@ -16,6 +16,19 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("PBF_OFFLOAD_ARCH", "gfx950")
 
 
+def source_digest() -> str:
+    """sha256 over the library's sources and compile flags: identifies the kernels a measurement
+    (e.g. the committed PMC traffic summary) was taken on, independent of rebuilds."""
+    import hashlib
+    h = hashlib.sha256()
+    for d in sorted(DEPS):
+        h.update(os.path.basename(d).encode())
+        with open(d, "rb") as fh:
+            h.update(fh.read())
+    h.update(ARCH.encode())
+    return h.hexdigest()
+
+
 def up_to_date() -> bool:
     if not os.path.exists(LIB):
         return False

@@ -49,7 +49,7 @@ def pass_of(kernel: str) -> str | None:
         return "probe" if args[2].strip() == "true" else "build"
     if kernel in ("pbf::k_tile_build", "pbf::k_ovf_build"):
         return "build"
-    if kernel in ("pbf::k_tile_probe", "pbf::k_gather", "pbf::k_gather_ring"):
+    if kernel in ("pbf::k_tile_probe", "pbf::k_gather", "pbf::k_gather_ring", "pbf::k_hw_to_hitmask"):
         return "probe"
     return None
 
@@ -74,12 +74,11 @@ def main() -> None:
         agg["write_bytes"] += wr
     for p in res["passes"].values():
         p["traffic_bytes"] = p["read_bytes"] + p["write_bytes"]
-    # the library these counters were taken on (bench.py only uses a summary of its own build)
-    import hashlib
+    # the kernels these counters were taken on (bench.py only uses a summary of its own sources)
     import os
-    lib = os.environ.get("PBF_LIB") or os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
-                                                   "pebbledb_amd", "libpebblebloom.so")
-    res["lib_sha256"] = hashlib.sha256(open(lib, "rb").read()).hexdigest()
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from pebbledb_amd.build import source_digest
+    res["source_sha256"] = source_digest()
     json.dump(res, open(out, "w"), indent=1)
     for k, v in res["kernels"].items():
         print(f"{k:45s} {v['pass']:6s} read {v['read_bytes'] / 1e6:9.1f} MB  write {v['write_bytes'] / 1e6:9.1f} MB")
