@@ -284,7 +284,8 @@ int run_atomic(pbf_filter_t* f, const Batch& b) {
 struct PartPlan {
     PartGeom pg;
     size_t lds_part;
-    size_t lds_gather;  // probes
+    size_t lds_gather;  // probes: per gather workgroup
+    uint32_t gsplit;    // probes: gather splits over tile ranges (grid G x gsplit)
 };
 
 // Partition strategy: PBF_PART=sort|ring forces one (tests, measurements); default auto.
@@ -316,6 +317,18 @@ uint32_t ring_entries(uint32_t B, uint32_t k, bool probe, uint32_t tb) {
     return uint64_t(kRingKeysPerSub) * k * 4 <= uint64_t(B) * rc ? rc : 0;
 }
 
+// Gather LDS = the key bitmap of a partition workgroup + one u16 run-boundary row (`row`
+// entries) per tile of the split.  Splits start at gather_splits() and double (up to 64) while
+// the workgroup does not fit, so large batches stay in one pipeline.
+void set_gather(PartPlan& pl, uint32_t B, uint32_t row) {
+    const size_t kb = size_t((pl.pg.kpw + 31) / 32) * 4;
+    uint32_t S = gather_splits();
+    auto lds = [&](uint32_t sp) { return kb + size_t((B + sp - 1) / sp) * row * 2 + 16; };
+    while (lds(S) > 156 * 1024 && S < 64 && S < B) S *= 2;
+    pl.gsplit = S;
+    pl.lds_gather = lds(S);
+}
+
 PartPlan plan_ring(uint32_t B, uint32_t k, uint64_t n, uint32_t rc, double share) {
     PartPlan pl{};
     const uint64_t kps = kRingKeysPerSub;
@@ -332,7 +345,7 @@ PartPlan plan_ring(uint32_t B, uint32_t k, uint64_t n, uint32_t rc, double share
     const uint64_t cap = uint64_t(mu + 8.0 * std::sqrt(mu) + 32.0);
     pl.pg.cap = uint32_t(((cap + 31) / 32) * 32);
     pl.lds_part = size_t((2 * B + 16 * 128 + 3) & ~3u) * 4 + size_t(B) * rc * 4;
-    pl.lds_gather = size_t((kpw + 31) / 32) * 4 + size_t(B) * (pl.pg.nq + 1) * 2 + 16;
+    set_gather(pl, B, pl.pg.nq + 1);
     return pl;
 }
 
@@ -356,7 +369,7 @@ PartPlan plan_partition(uint32_t B, uint32_t k, int km, uint64_t n, bool probe, 
     const double mu = double(kpw) * k * share;
     const uint64_t cap = uint64_t(mu + 8.0 * std::sqrt(mu) + 32.0);
     pl.pg.cap = uint32_t(((cap + 31) / 32) * 32);
-    pl.lds_gather = size_t((pl.pg.kpw + 31) / 32) * 4 + size_t(B) * (pl.pg.nsub + 1) * 2 + 16;
+    set_gather(pl, B, pl.pg.nsub + 1);
     return pl;
 }
 
@@ -466,10 +479,8 @@ int run_tiled_probe_set(pbf_filter_t* f, pbf_filter_t* const* fs, uint32_t nf, c
     auto* R = static_cast<uint32_t*>(f->rbits.p);
     auto* neg = static_cast<uint32_t*>(f->neg.p);
     hipStream_t s = f->stream;
-    // ring gather split over S tile ranges (several small workgroups per CU)
-    const uint32_t S = pg.ring ? gather_splits() : 1;
-    const size_t lds_gather_split =
-        pg.ring ? size_t((pg.kpw + 31) / 32) * 4 + size_t((B + S - 1) / S) * (pg.nq + 1) * 2 + 16 : pl.lds_gather;
+    // gather split over S tile ranges (several small workgroups per CU)
+    const uint32_t S = pl.gsplit;
     uint32_t* hw = nullptr;
     if (S > 1) {
         HIP_TRY(f->hw.ensure(neg_bytes));
@@ -512,26 +523,24 @@ int run_tiled_probe_set(pbf_filter_t* f, pbf_filter_t* const* fs, uint32_t nf, c
         });
         HIP_TRY(err);
         CHECK_LAUNCH();
-        if (pg.ring) HIP_TRY(allow_lds(k_gather_ring, lds_gather_split));
+        if (pg.ring) HIP_TRY(allow_lds(k_gather_ring, pl.lds_gather));
         else HIP_TRY(allow_lds(k_gather, pl.lds_gather));
         for (uint32_t i = 0; i < nf; ++i) {
             if (S > 1) HIP_TRY(hipMemsetAsync(hw, 0xFF, neg_bytes, s));
             k_tile_probe<<<B, 1024, lds_tile, s>>>(tm, pg, regions, fill, fs[i]->bitmap, R, expand);
             CHECK_LAUNCH();
             const uint32_t* negi = neg + i * neg_words;
+            const dim3 grid(pg.G, S);
             if (pg.ring)
-            {
-                const dim3 grid(pg.G, S);
-                k_gather_ring<<<grid, 512, lds_gather_split, s>>>(tm, pg, b.n, regions, R, fill, subcnt, negi, alive,
-                                                                 outs[i] + hm_off, hw);
-                if (S > 1) {
-                    CHECK_LAUNCH();
-                    k_hw_to_hitmask<<<grid_for(neg_words, 256, 4096), 256, 0, s>>>(hw, b.n, outs[i] + hm_off);
-                }
-            }
+                k_gather_ring<<<grid, 512, pl.lds_gather, s>>>(tm, pg, b.n, regions, R, fill, subcnt, negi, alive,
+                                                              outs[i] + hm_off, hw);
             else
-                k_gather<<<pg.G, 1024, pl.lds_gather, s>>>(tm, pg, b.n, regions, R, subcnt, negi, outs[i] + hm_off);
+                k_gather<<<grid, 512, pl.lds_gather, s>>>(tm, pg, b.n, regions, R, subcnt, negi, outs[i] + hm_off, hw);
             CHECK_LAUNCH();
+            if (S > 1) {
+                k_hw_to_hitmask<<<grid_for(neg_words, 256, 4096), 256, 0, s>>>(hw, b.n, outs[i] + hm_off);
+                CHECK_LAUNCH();
+            }
         }
         return PBF_OK;
     };

@@ -354,18 +354,4 @@ __global__ void __launch_bounds__(512) k_gather_ring(TileMap tm, PartGeom pg, ui
     }
 }
 
-// hw (ANDed gather words, one per 32 keys) → the LSB-first hit mask of n keys.
-__global__ void k_hw_to_hitmask(const uint32_t* __restrict__ hw, uint64_t n, uint8_t* __restrict__ hitmask) {
-    const uint64_t nw = (n + 31) / 32;
-    for (uint64_t w = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; w < nw; w += uint64_t(gridDim.x) * blockDim.x) {
-        const uint64_t key0 = w * 32;
-        const uint32_t bits = hw[w];
-        const uint64_t nbt = min<uint64_t>(4, (n - key0 + 7) / 8);
-        if (nbt == 4 && (reinterpret_cast<uintptr_t>(hitmask + key0 / 8) & 3) == 0)
-            *reinterpret_cast<uint32_t*>(hitmask + key0 / 8) = bits;
-        else
-            for (uint64_t q = 0; q < nbt; ++q) hitmask[key0 / 8 + q] = uint8_t(bits >> (8 * q));
-    }
-}
-
 }  // namespace pbf

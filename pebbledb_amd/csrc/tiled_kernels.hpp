@@ -502,21 +502,24 @@ __global__ void __launch_bounds__(1024) k_tile_probe(TileMap tm, PartGeom pg, co
 // g*kpw + j*kps + slot.  A 0 result bit clears the key's bit in an LDS bitmap of the
 // workgroup's keys, which is finally written out as hit-mask words.
 //   LDS: pref[B][nsub+1] (u16 run boundaries, region-relative), kbits[kpw/32].
-__global__ void __launch_bounds__(1024) k_gather(TileMap tm, PartGeom pg, uint64_t n,
-                                                 const uint32_t* __restrict__ regions, const uint32_t* __restrict__ R,
-                                                 const uint32_t* __restrict__ subcnt, const uint32_t* __restrict__ neg,
-                                                 uint8_t* __restrict__ hitmask) {
+__global__ void __launch_bounds__(512) k_gather(TileMap tm, PartGeom pg, uint64_t n,
+                                                const uint32_t* __restrict__ regions, const uint32_t* __restrict__ R,
+                                                const uint32_t* __restrict__ subcnt, const uint32_t* __restrict__ neg,
+                                                uint8_t* __restrict__ hitmask, uint32_t* __restrict__ hw) {
     extern __shared__ uint32_t smem[];
     const uint32_t B = tm.nbuckets, cap = pg.cap, wpr = cap / 32, nsub = pg.nsub;
     const uint32_t tid = threadIdx.x, nt = blockDim.x;
     const uint32_t lane = tid & 63, wave = tid >> 6, nwaves = nt >> 6;
     const uint32_t g = blockIdx.x;
+    // split sp of S takes tiles [b_lo, b_hi) (as k_gather_ring)
+    const uint32_t S = gridDim.y, sp = blockIdx.y;
+    const uint32_t b_lo = uint32_t(uint64_t(B) * sp / S), b_hi = uint32_t(uint64_t(B) * (sp + 1) / S);
     const uint64_t k0 = uint64_t(g) * pg.kpw;
     const uint64_t k1 = min(n, k0 + pg.kpw);
     const uint32_t nkeys = uint32_t(k1 - k0);
     const uint32_t kw = uint32_t((pg.kpw + 31) / 32);
     uint32_t* kbits = smem;                                    // kw words
-    uint16_t* pref = reinterpret_cast<uint16_t*>(kbits + kw);  // B * (nsub + 1)
+    uint16_t* pref = reinterpret_cast<uint16_t*>(kbits + kw);  // (b_hi - b_lo) * (nsub + 1)
     const uint32_t ps = nsub + 1;
     // key bits: 1 for this workgroup's keys not already refuted by an overflow entry
     for (uint32_t w = tid; w < kw; w += nt) {
@@ -530,9 +533,10 @@ __global__ void __launch_bounds__(1024) k_gather(TileMap tm, PartGeom pg, uint64
     }
     // run boundaries per tile: pref[b][j] = in-region entries of (g, b) before sub-chunk j
     const uint32_t* sc = subcnt + uint64_t(g) * nsub * B;
-    for (uint32_t b = tid; b < B; b += nt) {
+    for (uint32_t b = b_lo + tid; b < b_hi; b += nt) {
+        uint16_t* pr = pref + (b - b_lo) * ps;
         uint32_t run = 0;
-        pref[b * ps] = 0;
+        pr[0] = 0;
         for (uint32_t j0 = 0; j0 < nsub; j0 += 8) {
             uint32_t c[8];
 #pragma unroll
@@ -541,7 +545,7 @@ __global__ void __launch_bounds__(1024) k_gather(TileMap tm, PartGeom pg, uint64
             for (int u = 0; u < 8; ++u) {
                 if (j0 + u < nsub) {
                     run = min(run + c[u], cap);
-                    pref[b * ps + j0 + u + 1] = uint16_t(run);
+                    pr[j0 + u + 1] = uint16_t(run);
                 }
             }
         }
@@ -550,10 +554,11 @@ __global__ void __launch_bounds__(1024) k_gather(TileMap tm, PartGeom pg, uint64
     // one wave per region, 256 entries (one 16-byte load per lane) per step; U regions in
     // flight per wave.  Regions start 128-B aligned (cap is a multiple of 32).
     constexpr int U = 4;
-    for (uint32_t b0 = wave; b0 < B; b0 += nwaves * U) {
+    for (uint32_t b0 = b_lo + wave; b0 < b_hi; b0 += nwaves * U) {
         uint32_t fillb[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) fillb[u] = b0 + u * nwaves < B ? uint32_t(pref[(b0 + u * nwaves) * ps + nsub]) : 0u;
+        for (int u = 0; u < U; ++u)
+            fillb[u] = b0 + u * nwaves < b_hi ? uint32_t(pref[(b0 + u * nwaves - b_lo) * ps + nsub]) : 0u;
         uint32_t maxf = 0;
 #pragma unroll
         for (int u = 0; u < U; ++u) maxf = max(maxf, fillb[u]);
@@ -562,7 +567,7 @@ __global__ void __launch_bounds__(1024) k_gather(TileMap tm, PartGeom pg, uint64
             uint32_t rw[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                const uint32_t b = min(b0 + u * nwaves, B - 1);
+                const uint32_t b = min(b0 + u * nwaves, b_hi - 1);
                 const uint32_t r = min(r0 + lane * 4, (max(fillb[u], 1u) - 1) & ~3u);
                 const uint64_t reg = uint64_t(g) * B + b;
                 v[u] = *reinterpret_cast<const uint4*>(regions + reg * cap + r);
@@ -572,12 +577,12 @@ __global__ void __launch_bounds__(1024) k_gather(TileMap tm, PartGeom pg, uint64
             for (int u = 0; u < U; ++u) {
                 const uint32_t b = b0 + u * nwaves;
                 const uint32_t r = r0 + lane * 4;
-                if (b < B && r < fillb[u]) {
+                if (b < b_hi && r < fillb[u]) {
                     uint32_t fails = ~r_quad(rw[u], r) & 0xFu;
                     if (fillb[u] - r < 4) fails &= (1u << (fillb[u] - r)) - 1u;
                     if (fails) {
                         // sub-chunk of position r: the last j with pref[b][j] <= r
-                        const uint16_t* pb = pref + b * ps;
+                        const uint16_t* pb = pref + (b - b_lo) * ps;
                         uint32_t lo = 0, len = nsub;
                         while (len > 1) {
                             const uint32_t half = len >> 1;
@@ -599,6 +604,10 @@ __global__ void __launch_bounds__(1024) k_gather(TileMap tm, PartGeom pg, uint64
         }
     }
     lds_barrier();
+    if (S > 1) {  // AND this split's words into hw (k_hw_to_hitmask writes the hit mask)
+        for (uint32_t w = tid; w * 32 < nkeys; w += nt) atomicAnd(hw + (k0 >> 5) + w, kbits[w]);
+        return;
+    }
     // hit-mask words for keys [k0, k1): k0 is a multiple of 64
     for (uint32_t w = tid; w * 32 < nkeys; w += nt) {
         const uint64_t key0 = k0 + uint64_t(w) * 32;
@@ -608,6 +617,20 @@ __global__ void __launch_bounds__(1024) k_gather(TileMap tm, PartGeom pg, uint64
             *reinterpret_cast<uint32_t*>(hitmask + key0 / 8) = bits;
         else
             for (uint64_t q = 0; q < nb; ++q) hitmask[key0 / 8 + q] = uint8_t(bits >> (8 * q));
+    }
+}
+
+// hw (ANDed gather words, one per 32 keys) → the LSB-first hit mask of n keys.
+__global__ void k_hw_to_hitmask(const uint32_t* __restrict__ hw, uint64_t n, uint8_t* __restrict__ hitmask) {
+    const uint64_t nw = (n + 31) / 32;
+    for (uint64_t w = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; w < nw; w += uint64_t(gridDim.x) * blockDim.x) {
+        const uint64_t key0 = w * 32;
+        const uint32_t bits = hw[w];
+        const uint64_t nbt = min<uint64_t>(4, (n - key0 + 7) / 8);
+        if (nbt == 4 && (reinterpret_cast<uintptr_t>(hitmask + key0 / 8) & 3) == 0)
+            *reinterpret_cast<uint32_t*>(hitmask + key0 / 8) = bits;
+        else
+            for (uint64_t q = 0; q < nbt; ++q) hitmask[key0 / 8 + q] = uint8_t(bits >> (8 * q));
     }
 }
 
