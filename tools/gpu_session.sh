@@ -27,9 +27,15 @@ for step in "$@"; do
     bench_c5) run bench_c5 600 python bench.py --config c5 --steps 5 --warmup 2 ;;
     prof_c34) run prof_c4 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_c4 -o run -- python bench.py --config c4 --steps 2 --warmup 1
               python tools/prof_summary.py gpurun_out/prof_c4 > gpurun_out/prof_c4_summary.txt 2>&1
-              run prof_c3 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_c3 -o run -- python bench.py --config c3 --steps 3 --warmup 1 --no-cpu-baseline
+              ;;
+    prof_c3) run prof_c3 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_c3 -o run -- python bench.py --config c3 --steps 3 --warmup 1 --no-cpu-baseline
               python tools/prof_summary.py gpurun_out/prof_c3 > gpurun_out/prof_c3_summary.txt 2>&1 ;;
     gsplit) for sp in ${PBF_SPLITS:-8 12 16}; do PBF_GATHER_SPLIT=$sp run gsplit_$sp 300 python bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-host-inclusive; done ;;
+    screen) PBF_PROBE_ROUNDS=2 run screen_tests 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_device_resident.py -m gpu -x -v -rf --timeout 300 --timeout-method thread -k "strategies or config2 or device_resident_equals or splitmix or sweep or incremental or tails or golden"
+            PBF_PROBE_ROUNDS=2 run screen_bench 300 python bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-host-inclusive
+            run noscreen_bench 300 python bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-host-inclusive ;;
+    prof_screen) PBF_PROBE_ROUNDS=2 run prof_screen 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_screen -o run -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-host-inclusive
+                 python tools/prof_summary.py gpurun_out/prof_screen > gpurun_out/prof_screen_summary.txt 2>&1 ;;
     bench_atomic) run bench_atomic 600 python bench.py --steps 10 --warmup 3 --build-mode 1 --no-cpu-baseline ;;
     bench_tt) run bench_tt 300 python bench.py --steps 20 --warmup 5 --build-mode 2 --probe-mode 2 --no-cpu-baseline --no-host-inclusive ;;
     bench_modes) for bm in 1 2; do for pm in 1 2; do run bench_b${bm}_p${pm} 300 python bench.py --steps 20 --warmup 5 --build-mode $bm --probe-mode $pm --no-cpu-baseline; done; done ;;
