@@ -192,7 +192,7 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
                         const uint32_t tb = d & 0xFFFu;
                         const uint32_t e = (d >> 12) + q * 4;  // region position
                         const uint4 v = *reinterpret_cast<const uint4*>(ring + tb * RC + (e & rmask));
-                        *reinterpret_cast<uint4*>(regions + (uint64_t(g) * B + tb) * cap + e) = v;
+                        *reinterpret_cast<uint4*>(regions + region_id(g, tb, pg.G, B) * cap + e) = v;
                     }
                 }
                 __builtin_amdgcn_wave_barrier();
@@ -226,7 +226,7 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
                     const uint32_t tb = d & 0xFFFu;
                     const uint32_t e = (d >> 12) + q * 4;
                     const uint4 v = *reinterpret_cast<const uint4*>(ring + tb * RC + (e & rmask));
-                    *reinterpret_cast<uint4*>(regions + (uint64_t(g) * B + tb) * cap + e) = v;
+                    *reinterpret_cast<uint4*>(regions + region_id(g, tb, pg.G, B) * cap + e) = v;
                 }
             }
             __builtin_amdgcn_wave_barrier();
@@ -302,7 +302,7 @@ __global__ void __launch_bounds__(512) k_gather_ring(TileMap tm, PartGeom pg, ui
             for (int u = 0; u < U; ++u) {
                 const uint32_t b = min(b0 + u * nwaves, b_hi - 1);
                 const uint32_t r = min(r0 + lane * 4, (max(fillb[u], 1u) - 1) & ~3u);
-                const uint64_t reg = uint64_t(g) * B + b;
+                const uint64_t reg = region_id(g, b, pg.G, B);
                 v[u] = *reinterpret_cast<const uint4*>(regions + reg * cap + r);
                 rw[u] = R[reg * wpr + (r >> 5)];
             }

@@ -63,6 +63,17 @@ __device__ __forceinline__ void spill_probe(const ProbeSet& ps, uint64_t bit, ui
             atomicOr(ps.neg + f * ps.neg_stride + (key >> 5), 1u << (key & 31));
 }
 
+// Region (g, b) = partition workgroup g's entries of tile b.  PBF_REGION_TILE_MAJOR lays the
+// regions out tile-major (a tile's G regions back to back: contiguous for the tile passes) instead
+// of workgroup-major (a workgroup's B regions back to back: contiguous for the gather).
+__device__ __forceinline__ uint64_t region_id(uint32_t g, uint32_t b, uint32_t G, uint32_t B) {
+#ifdef PBF_REGION_TILE_MAJOR
+    return uint64_t(b) * G + g;
+#else
+    return uint64_t(g) * B + b;
+#endif
+}
+
 struct PartGeom {
     uint32_t G;        // partition workgroups
     uint32_t cap;      // region capacity in entries (multiple of 32)
@@ -287,7 +298,7 @@ __global__ void __launch_bounds__(kPartThreads) k_part(KeySet ks, uint64_t n, in
                 const uint32_t r = cursor[b[u]] + e;
                 if (e < tot) {
                     if (r < pg.cap) {
-                        regions[(uint64_t(g) * B + b[u]) * pg.cap + r] = v[u];
+                        regions[region_id(g, b[u], pg.G, B) * pg.cap + r] = v[u];
                     } else if constexpr (PROBE) {
                         spill_probe(ps, pos_to_bit((b[u] << tm.tb) | (v[u] & lmask), tm), s0 + (v[u] >> kSlotShift));
                     } else {
@@ -376,7 +387,10 @@ __global__ void __launch_bounds__(1024) k_tile_build(TileMap tm, PartGeom pg, co
     lds_barrier();
     const uint32_t lane = tid & 63, wave = tid >> 6, nwaves = nt >> 6;
     const uint32_t lmask = (1u << tm.tb) - 1u;
-    constexpr int U = 4;
+#ifndef PBF_TB_U
+#define PBF_TB_U 4
+#endif
+    constexpr int U = PBF_TB_U;  // regions of loads in flight per wave
     for (uint32_t g0 = wave; g0 < G; g0 += nwaves * U) {
         uint4 v[U];
         uint32_t f[U];
@@ -386,7 +400,7 @@ __global__ void __launch_bounds__(1024) k_tile_build(TileMap tm, PartGeom pg, co
             f[u] = q < G ? fills[q] : 0u;
             // unconditional loads, clamped to the filled part (idle lanes re-read its last line)
             const uint32_t lc = min(lane, (max(f[u], 1u) - 1) >> 2);
-            v[u] = reinterpret_cast<const uint4*>(regions + (uint64_t(min(q, G - 1)) * B + b) * cap)[lc];
+            v[u] = reinterpret_cast<const uint4*>(regions + region_id(min(q, G - 1), b, G, B) * cap)[lc];
         }
 #pragma unroll
         for (int u = 0; u < U; ++u)
@@ -397,7 +411,7 @@ __global__ void __launch_bounds__(1024) k_tile_build(TileMap tm, PartGeom pg, co
         for (uint32_t q = wave; q < G; q += nwaves) {
             const uint32_t fq = fills[q];
             for (uint32_t c = 64 + lane; c * 4 < fq; c += 64)
-                or_bits4(tile, reinterpret_cast<const uint4*>(regions + (uint64_t(q) * B + b) * cap)[c], c * 4, fq,
+                or_bits4(tile, reinterpret_cast<const uint4*>(regions + region_id(q, b, G, B) * cap)[c], c * 4, fq,
                          lmask);
         }
     }
@@ -470,7 +484,7 @@ __global__ void __launch_bounds__(1024) k_tile_probe(TileMap tm, PartGeom pg, co
             const uint32_t c = min(c0 + u * stride + wsub, total - 1);  // unconditional loads
             qq[u] = expand ? uint32_t(wq[c]) : bucket_of(wpre, G, c);
             word[u] = c - wpre[qq[u]];
-            v[u] = reinterpret_cast<const uint4*>(regions + (uint64_t(qq[u]) * B + b) * cap + word[u] * 32)[l];
+            v[u] = reinterpret_cast<const uint4*>(regions + region_id(qq[u], b, G, B) * cap + word[u] * 32)[l];
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -488,7 +502,7 @@ __global__ void __launch_bounds__(1024) k_tile_probe(TileMap tm, PartGeom pg, co
             const uint64_t m0 = __ballot(t0), m1 = __ballot(t1), m2 = __ballot(t2), m3 = __ballot(t3);
             if (l == 0 && c < total) {
                 const uint32_t sh = wsub * 8;
-                R[(uint64_t(qq[u]) * B + b) * wpr + word[u]] =
+                R[region_id(qq[u], b, G, B) * wpr + word[u]] =
                     uint32_t((m0 >> sh) & 0xFF) | (uint32_t((m1 >> sh) & 0xFF) << 8) |
                     (uint32_t((m2 >> sh) & 0xFF) << 16) | (uint32_t((m3 >> sh) & 0xFF) << 24);
             }
@@ -569,7 +583,7 @@ __global__ void __launch_bounds__(512) k_gather(TileMap tm, PartGeom pg, uint64_
             for (int u = 0; u < U; ++u) {
                 const uint32_t b = min(b0 + u * nwaves, b_hi - 1);
                 const uint32_t r = min(r0 + lane * 4, (max(fillb[u], 1u) - 1) & ~3u);
-                const uint64_t reg = uint64_t(g) * B + b;
+                const uint64_t reg = region_id(g, b, pg.G, B);
                 v[u] = *reinterpret_cast<const uint4*>(regions + reg * cap + r);
                 rw[u] = R[reg * wpr + (r >> 5)];
             }

@@ -36,6 +36,7 @@ for step in "$@"; do
             run noscreen_bench 300 python bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-host-inclusive ;;
     prof_screen) PBF_PROBE_ROUNDS=2 run prof_screen 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_screen -o run -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-host-inclusive
                  python tools/prof_summary.py gpurun_out/prof_screen > gpurun_out/prof_screen_summary.txt 2>&1 ;;
+    pytest_both) PBF_LIB=$PWD/build/variants/both.so run pytest_both 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_device_resident.py -m gpu -x -q -rf --timeout 300 --timeout-method thread -k "strategies or config2 or device_resident_equals or sweep or golden" ;;
     bench_atomic) run bench_atomic 600 python bench.py --steps 10 --warmup 3 --build-mode 1 --no-cpu-baseline ;;
     bench_tt) run bench_tt 300 python bench.py --steps 20 --warmup 5 --build-mode 2 --probe-mode 2 --no-cpu-baseline --no-host-inclusive ;;
     bench_modes) for bm in 1 2; do for pm in 1 2; do run bench_b${bm}_p${pm} 300 python bench.py --steps 20 --warmup 5 --build-mode $bm --probe-mode $pm --no-cpu-baseline; done; done ;;
