@@ -37,6 +37,16 @@ for step in "$@"; do
     prof_screen) PBF_PROBE_ROUNDS=2 run prof_screen 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_screen -o run -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-host-inclusive
                  python tools/prof_summary.py gpurun_out/prof_screen > gpurun_out/prof_screen_summary.txt 2>&1 ;;
     pytest_both) PBF_LIB=$PWD/build/variants/both.so run pytest_both 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_device_resident.py -m gpu -x -q -rf --timeout 300 --timeout-method thread -k "strategies or config2 or device_resident_equals or sweep or golden" ;;
+    final) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+           run pytest 900 python -u -m pytest tests -m gpu -x -v -rf --timeout 300 --timeout-method thread
+           run bench 600 python bench.py --steps 20 --warmup 5
+           run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline
+           python tools/prof_summary.py gpurun_out/prof > gpurun_out/prof_summary.txt 2>&1
+           run pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_fetch -o run -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-host-inclusive
+           run pmc_write 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_write -o run -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-host-inclusive
+           run bench_c3 600 python bench.py --config c3 --steps 5 --warmup 2 --no-cpu-baseline
+           run bench_c4 600 python bench.py --config c4 --steps 3 --warmup 1
+           run bench_c5 600 python bench.py --config c5 --steps 5 --warmup 2 ;;
     bench_atomic) run bench_atomic 600 python bench.py --steps 10 --warmup 3 --build-mode 1 --no-cpu-baseline ;;
     bench_tt) run bench_tt 300 python bench.py --steps 20 --warmup 5 --build-mode 2 --probe-mode 2 --no-cpu-baseline --no-host-inclusive ;;
     bench_modes) for bm in 1 2; do for pm in 1 2; do run bench_b${bm}_p${pm} 300 python bench.py --steps 20 --warmup 5 --build-mode $bm --probe-mode $pm --no-cpu-baseline; done; done ;;
