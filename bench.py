@@ -173,6 +173,14 @@ def host_inclusive(bf, keys, n, nb_bytes, L, torch, np, reps=3):
     }
 
 
+def all_reduce_scalar(torch, dist, value, op, dtype):
+    """max / min of a scalar over ranks (RCCL: a device tensor; gloo rehearsal: a host one)."""
+    dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([value], dtype=dtype, device=dev)
+    dist.all_reduce(t, op=op)
+    return t.item()
+
+
 def sets_main(args, rank, world, local, torch, dist, np):
     """Configs 4 and 5: eight independent SSTable filters spread over the ranks (8/N each,
     shard.filters_for_rank), no collective on the data path.
@@ -293,12 +301,8 @@ def sets_main(args, rank, world, local, torch, dist, np):
             cnt = per if g < 7 else half - 7 * per
             ok &= bool(bits[g * per:g * per + cnt].all())
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        okt = torch.tensor([1 if ok else 0], dtype=torch.int32, device="cuda")
-        dist.all_reduce(okt, op=dist.ReduceOp.MIN)
-        ok = bool(okt.item())
+        elapsed = float(all_reduce_scalar(torch, dist, elapsed, dist.ReduceOp.MAX, torch.float64))
+        ok = bool(all_reduce_scalar(torch, dist, 1 if ok else 0, dist.ReduceOp.MIN, torch.int32))
     if rank == 0:
         ms = elapsed / args.steps * 1e3
         if args.config == "c4":
@@ -352,6 +356,11 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal of the N-rank path on a one-GPU box: every rank on device PBF_BENCH_DEVICE,
+    # rendezvous / max-over-ranks over gloo (PBF_BENCH_BACKEND=gloo); the driver's runs use
+    # one GPU per rank over RCCL
+    if os.environ.get("PBF_BENCH_DEVICE"):
+        local = int(os.environ["PBF_BENCH_DEVICE"])
     if world != args.gpus:
         print(f"warning: WORLD_SIZE={world} but --gpus={args.gpus}", file=sys.stderr)
 
@@ -361,7 +370,11 @@ def main():
 
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group(backend="nccl", init_method="env://", device_id=torch.device("cuda", local))
+        backend = os.environ.get("PBF_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group(backend="nccl", init_method="env://", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend=backend, init_method="env://")
 
     if args.config in ("c4", "c5"):
         sets_main(args, rank, world, local, torch, dist, np)
@@ -463,12 +476,8 @@ def main():
     build_ms = sum(e[0].elapsed_time(e[1]) for e in events) / len(events)
     probe_ms = sum(e[1].elapsed_time(e[2]) for e in events) / len(events)
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        ok = torch.tensor([1 if members_ok else 0], dtype=torch.int32, device="cuda")
-        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-        members_ok = bool(ok.item())
+        elapsed = float(all_reduce_scalar(torch, dist, elapsed, dist.ReduceOp.MAX, torch.float64))
+        members_ok = bool(all_reduce_scalar(torch, dist, 1 if members_ok else 0, dist.ReduceOp.MIN, torch.int32))
 
     host_inc = None
     if rank == 0 and offs is None and not args.no_host_inclusive:

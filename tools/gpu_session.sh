@@ -47,6 +47,12 @@ for step in "$@"; do
            run bench_c3 600 python bench.py --config c3 --steps 5 --warmup 2 --no-cpu-baseline
            run bench_c4 600 python bench.py --config c4 --steps 3 --warmup 1
            run bench_c5 600 python bench.py --config c5 --steps 5 --warmup 2 ;;
+    rehearse) export PBF_BENCH_DEVICE=0 PBF_BENCH_BACKEND=gloo
+              run rh_c2_n2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 10 --warmup 3
+              run rh_c2_n4 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29512 bench.py --gpus 4 --steps 10 --warmup 3
+              run rh_c5_n2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29513 bench.py --gpus 2 --config c5 --steps 3 --warmup 1
+              run rh_c4_n2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29514 bench.py --gpus 2 --config c4 --steps 2 --warmup 1
+              unset PBF_BENCH_DEVICE PBF_BENCH_BACKEND ;;
     bench_atomic) run bench_atomic 600 python bench.py --steps 10 --warmup 3 --build-mode 1 --no-cpu-baseline ;;
     bench_tt) run bench_tt 300 python bench.py --steps 20 --warmup 5 --build-mode 2 --probe-mode 2 --no-cpu-baseline --no-host-inclusive ;;
     bench_modes) for bm in 1 2; do for pm in 1 2; do run bench_b${bm}_p${pm} 300 python bench.py --steps 20 --warmup 5 --build-mode $bm --probe-mode $pm --no-cpu-baseline; done; done ;;
