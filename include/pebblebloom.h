@@ -128,6 +128,20 @@ int pbf_last_build_mode(pbf_filter_t* f);
 int pbf_set_probe_mode(pbf_filter_t* f, int mode);
 int pbf_last_probe_mode(pbf_filter_t* f);
 
+/* SSTableBuilder's data section (src/sstable.py:224-268; DataBlock.to_bytes blocks.py:33-37;
+ * Record.to_bytes record.py:66-72, key_size = the key's UTF-8 CHARACTER count as the reference's
+ * len(str), record.py:24).  Record i = (keys[key_offsets[i], key_offsets[i+1]),
+ * values[value_offsets[i], value_offsets[i+1])).  The caller plans the blocks with the
+ * DataBlockBuilder rule (blocks.py:78-95; pebbledb_amd/sstable_data.py plan_blocks): block b
+ * holds records [block_first[b], block_first[b+1]) (block_first has nblocks+1 entries, 0 .. n)
+ * and is written at byte block_out[b] of out (block_out[nblocks] = section size); a block's
+ * records may total at most 65536 bytes.  One workgroup per block assembles it in LDS.
+ * on_device = 0: all pointers are host memory (checked, staged, section copied back);
+ * on_device = 1: device pointers, the offsets start at the data pointers. Synchronous. */
+int pbf_encode_data_blocks(int device, const uint8_t* keys, const uint64_t* key_offsets, const uint8_t* values,
+                           const uint64_t* value_offsets, uint64_t n, const uint64_t* block_first,
+                           const uint64_t* block_out, uint64_t nblocks, uint8_t* out, int on_device);
+
 /* Synthetic keys straight into device memory (bench / tests; definitions in
  * pebbledb_amd/keys.py): 16 hex chars of splitmix64(seed + start + i), and the variable-length
  * 8..64-byte family (offsets must already hold the n+1 offsets, relative to offsets[0]). */

@@ -51,6 +51,7 @@ SIGNATURES = {
     "pbf_last_build_mode": (_int, [_vp]),
     "pbf_set_probe_mode": (_int, [_vp, _int]),
     "pbf_last_probe_mode": (_int, [_vp]),
+    "pbf_encode_data_blocks": (_int, [_int, _u8p, _vp, _u8p, _vp, _u64, _vp, _vp, _u64, _u8p, _int]),
     "pbf_gen_splitmix_hex": (_int, [_int, _vp, _u8p, _u64, _u64, _u64]),
     "pbf_gen_varlen": (_int, [_int, _vp, _u8p, _vp, _u64, _u64, _u64]),
     "pbf_last_error": (ctypes.c_char_p, []),

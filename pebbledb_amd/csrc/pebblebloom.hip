@@ -25,6 +25,7 @@
 #include "bloom_kernels.hpp"
 #include "tiled_kernels.hpp"
 #include "ring_kernels.hpp"
+#include "sstable_kernels.hpp"
 
 using namespace pbf;
 
@@ -919,6 +920,22 @@ __global__ void k_popcount(const uint32_t* __restrict__ w, uint64_t n, unsigned 
     if (threadIdx.x == 0) atomicAdd(out, part[0] + part[1] + part[2] + part[3]);
 }
 
+// Scratch of pbf_encode_data_blocks, one per device (the encoder is not tied to a filter).
+struct EncodeCtx {
+    std::mutex mu;
+    hipStream_t stream = nullptr;
+    DevBuf keys, vals, offs, out, err;
+};
+
+EncodeCtx& encode_ctx(int device) {
+    static std::mutex mu;
+    static std::map<int, EncodeCtx*> ctx;
+    std::lock_guard<std::mutex> lock(mu);
+    auto& p = ctx[device];
+    if (!p) p = new EncodeCtx();
+    return *p;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1173,6 +1190,70 @@ int pbf_set_probe_mode(pbf_filter_t* f, int mode) {
 }
 
 int pbf_last_probe_mode(pbf_filter_t* f) { return f ? f->last_probe_mode : 0; }
+
+int pbf_encode_data_blocks(int device, const uint8_t* keys, const uint64_t* key_offsets, const uint8_t* values,
+                           const uint64_t* value_offsets, uint64_t n, const uint64_t* block_first,
+                           const uint64_t* block_out, uint64_t nblocks, uint8_t* out, int on_device) {
+    if (nblocks == 0) return PBF_OK;
+    if (!key_offsets || !value_offsets || !block_first || !block_out || !out)
+        return fail(PBF_ERR_INVALID, "null pointer");
+    HIP_TRY(hipSetDevice(device));
+    HIP_TRY(allow_lds(k_encode_blocks, kEncodeLds));
+    EncodeCtx& c = encode_ctx(device);
+    std::lock_guard<std::mutex> lock(c.mu);
+    if (!c.stream) HIP_TRY(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
+    HIP_TRY(c.err.ensure(4));
+    HIP_TRY(hipMemsetAsync(c.err.p, 0, 4, c.stream));
+    const uint8_t *dk = keys, *dv = values;
+    const uint64_t *dko = key_offsets, *dvo = value_offsets, *dbf = block_first, *dbo = block_out;
+    uint8_t* dout = out;
+    uint64_t out_bytes = 0;
+    if (!on_device) {
+        // the host plan is checked here: blocks cover records 0..n in order, each fits a block
+        if (block_first[0] != 0 || block_first[nblocks] != n || block_out[0] != 0)
+            return fail(PBF_ERR_INVALID, "block plan must cover records [0, n) from byte 0");
+        for (uint64_t b = 0; b < nblocks; ++b) {
+            const uint64_t r0 = block_first[b], r1 = block_first[b + 1];
+            if (r1 < r0) return fail(PBF_ERR_INVALID, "block plan not monotonic");
+            const uint64_t dl = (key_offsets[r1] - key_offsets[r0]) + (value_offsets[r1] - value_offsets[r0]) + 8 * (r1 - r0);
+            if (dl > kMaxBlockData) return fail(PBF_ERR_INVALID, "a block's records exceed 65536 bytes");
+            if (block_out[b + 1] - block_out[b] != dl + 2 * (r1 - r0) + 2)
+                return fail(PBF_ERR_INVALID, "block_out does not match the blocks' encoded sizes");
+        }
+        out_bytes = block_out[nblocks];
+        const uint64_t kb = key_offsets[n], vb = value_offsets[n];
+        HIP_TRY(c.keys.ensure(kb + 16));
+        HIP_TRY(c.vals.ensure(vb + 16));
+        HIP_TRY(c.offs.ensure((2 * (n + 1) + 2 * (nblocks + 1)) * 8));
+        HIP_TRY(c.out.ensure(out_bytes + 16));
+        auto* o = static_cast<uint64_t*>(c.offs.p);
+        if (kb) HIP_TRY(hipMemcpyAsync(c.keys.p, keys, kb, hipMemcpyHostToDevice, c.stream));
+        if (vb) HIP_TRY(hipMemcpyAsync(c.vals.p, values, vb, hipMemcpyHostToDevice, c.stream));
+        HIP_TRY(hipMemcpyAsync(o, key_offsets, (n + 1) * 8, hipMemcpyHostToDevice, c.stream));
+        HIP_TRY(hipMemcpyAsync(o + n + 1, value_offsets, (n + 1) * 8, hipMemcpyHostToDevice, c.stream));
+        HIP_TRY(hipMemcpyAsync(o + 2 * (n + 1), block_first, (nblocks + 1) * 8, hipMemcpyHostToDevice, c.stream));
+        HIP_TRY(hipMemcpyAsync(o + 2 * (n + 1) + nblocks + 1, block_out, (nblocks + 1) * 8, hipMemcpyHostToDevice,
+                               c.stream));
+        dk = static_cast<const uint8_t*>(c.keys.p);
+        dv = static_cast<const uint8_t*>(c.vals.p);
+        dko = o;
+        dvo = o + n + 1;
+        dbf = o + 2 * (n + 1);
+        dbo = o + 2 * (n + 1) + nblocks + 1;
+        dout = static_cast<uint8_t*>(c.out.p);
+    }
+    hipStream_t s = on_device ? nullptr : c.stream;
+    if (on_device) HIP_TRY(hipMemsetAsync(c.err.p, 0, 4, s));
+    k_encode_blocks<<<uint32_t(nblocks), 512, kEncodeLds, s>>>(dk, dko, dv, dvo, dbf, dbo, dout,
+                                                               static_cast<unsigned int*>(c.err.p));
+    CHECK_LAUNCH();
+    unsigned int err = 0;
+    HIP_TRY(hipMemcpyAsync(&err, c.err.p, 4, hipMemcpyDeviceToHost, s));
+    if (!on_device) HIP_TRY(hipMemcpyAsync(out, dout, out_bytes, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (err) return fail(PBF_ERR_INVALID, std::to_string(err) + " block(s) exceed 65536 data bytes; not written");
+    return PBF_OK;
+}
 
 int pbf_gen_splitmix_hex(int device, void* stream, uint8_t* out_dev, uint64_t seed, uint64_t start, uint64_t n) {
     HIP_TRY(hipSetDevice(device));

@@ -1,0 +1,124 @@
+"""SSTable build on the device: data blocks (``pbf_encode_data_blocks``), meta blocks and the
+bloom filter — the byte-identical counterpart of the reference's ``SSTableBuilder``
+(src/sstable.py:209-288) for a flushed / compacted run of records.
+
+Host side (this module): pack the records into the boundary layout (key bytes + u64 offsets,
+value bytes + u64 offsets), plan the data blocks with the reference's greedy rule
+(``DataBlockBuilder.add``, blocks.py:78-95: a record joins the block iff the block's record
+bytes stay <= block_size; offsets and count are not counted), and encode the meta blocks
+(blocks.py:126-133, a few bytes per 64 KiB block).  Device side: every data block is
+assembled in LDS by one workgroup and written once (csrc/sstable_kernels.hpp); the bloom
+filter of all keys (fp_rate 0.001, sstable.py:274) is built by the bloom kernels and its
+bitmap copied from HBM straight into the file buffer (sstable_bloom.encode_sstable).
+
+Reference quirks kept: Record.key_size and MetaBlock key sizes are ``len(str)`` — characters,
+not UTF-8 bytes (record.py:24, blocks.py:127,129).  Divergences (inputs the reference
+mishandles): a record larger than block_size raises ValueError (the reference drops it from
+the data silently, blocks.py:84-85, while keeping its key in the bloom filter); an empty
+record list raises ValueError (the reference fails in MetaBlock.to_bytes); block_size must be
+<= 65536 (the reference's u16 offsets, blocks.py:34, overflow beyond).
+"""
+from __future__ import annotations
+
+import ctypes
+import struct
+
+import numpy as np
+
+from . import _native
+from .keys import PackedKeys
+
+BLOCK_SIZE = 65_536  # SSTableBuilder default (sstable.py:215)
+RECORD_HEADER = 8    # two i32 sizes (record.py:66-72)
+
+
+def pack_values(values) -> tuple[np.ndarray, np.ndarray]:
+    """(bytes, u64 offsets[n+1]) of a list of bytes values."""
+    vals = values if isinstance(values, list) else list(values)
+    lens = np.fromiter(map(len, vals), dtype=np.int64, count=len(vals))
+    offs = np.zeros(len(vals) + 1, dtype=np.uint64)
+    np.cumsum(lens, out=offs[1:])
+    return np.frombuffer(b"".join(vals), dtype=np.uint8), offs
+
+
+def key_offsets(pk: PackedKeys) -> np.ndarray:
+    if pk.offsets is not None:
+        return pk.offsets
+    return np.arange(pk.n + 1, dtype=np.uint64) * np.uint64(pk.key_len)
+
+
+def plan_blocks(ko: np.ndarray, vo: np.ndarray, block_size: int = BLOCK_SIZE) -> tuple[np.ndarray, np.ndarray]:
+    """DataBlockBuilder's greedy blocks (blocks.py:78-95, sstable.py:224-244): (block_first
+    [nblocks+1] record indices, block_out [nblocks+1] byte offsets of the encoded blocks)."""
+    n = len(ko) - 1
+    if n <= 0:
+        raise ValueError("an SSTable needs at least one record (the reference fails in MetaBlock.to_bytes)")
+    if not 0 < block_size <= 65_536:
+        raise ValueError("block_size must be in (0, 65536]: DataBlock offsets are u16 (blocks.py:34)")
+    sizes = (np.diff(ko.astype(np.int64)) + np.diff(vo.astype(np.int64)) + RECORD_HEADER)
+    if int(sizes.max()) > block_size:
+        raise ValueError("a record is larger than block_size (the reference would drop it, blocks.py:84-85)")
+    P = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum(sizes, out=P[1:])
+    first = [0]
+    s = 0
+    while s < n:
+        # the largest e with P[e] - P[s] <= block_size: records s..e-1 fill the block
+        e = int(np.searchsorted(P, P[s] + block_size, side="right")) - 1
+        first.append(e)
+        s = e
+    bf = np.asarray(first, dtype=np.uint64)
+    cnt = np.diff(bf.astype(np.int64))
+    data_len = P[bf[1:].astype(np.int64)] - P[bf[:-1].astype(np.int64)]
+    bo = np.zeros(len(bf), dtype=np.uint64)
+    np.cumsum(data_len + 2 * cnt + 2, out=bo[1:])
+    return bf, bo
+
+
+def encode_data_blocks(pk: PackedKeys, vals: np.ndarray, vo: np.ndarray, block_first: np.ndarray,
+                       block_out: np.ndarray, device: int = 0) -> np.ndarray:
+    """The data section (every encoded DataBlock back to back), written by the device."""
+    ko = np.ascontiguousarray(key_offsets(pk), dtype=np.uint64)
+    vo = np.ascontiguousarray(vo, dtype=np.uint64)
+    bf = np.ascontiguousarray(block_first, dtype=np.uint64)
+    bo = np.ascontiguousarray(block_out, dtype=np.uint64)
+    out = np.empty(int(bo[-1]), dtype=np.uint8)
+    keys = pk.data if pk.data.size else np.zeros(1, np.uint8)
+    vals = vals if vals.size else np.zeros(1, np.uint8)
+    vp = ctypes.c_void_p
+    rc = _native.lib().pbf_encode_data_blocks(device, vp(keys.ctypes.data), vp(ko.ctypes.data), vp(vals.ctypes.data),
+                                              vp(vo.ctypes.data), pk.n, vp(bf.ctypes.data), vp(bo.ctypes.data),
+                                              len(bf) - 1, vp(out.ctypes.data), 0)
+    _native.check(rc, "pbf_encode_data_blocks")
+    return out
+
+
+def meta_blocks(keys: list[str], block_first: np.ndarray, block_out: np.ndarray) -> tuple[bytes, list]:
+    """MetaBlock.to_bytes of every block (blocks.py:126-133) and the (first, last, offset) list."""
+    parts, metas = [], []
+    for b in range(len(block_first) - 1):
+        first, last = keys[int(block_first[b])], keys[int(block_first[b + 1]) - 1]
+        off = int(block_out[b])
+        metas.append((first, last, off))
+        parts.append(struct.pack("H", len(first)) + first.encode("utf-8") + struct.pack("H", len(last)) +
+                     last.encode("utf-8") + struct.pack("i", off))
+    return b"".join(parts), metas
+
+
+def build_sstable(keys, values, block_size: int = BLOCK_SIZE, fp_rate: float = 0.001, device=None):
+    """The bytes SSTableBuilder(block_size=block_size) writes after add(k, v) for every record
+    and build() (sstable.py:270-288), plus the meta blocks and the device BloomFilter."""
+    from .bloom_filter import BloomFilter, _default_device
+    from .sstable_bloom import encode_sstable
+
+    dev = _default_device if device is None else int(device)
+    keys = keys if isinstance(keys, list) else list(keys)
+    pk = PackedKeys.from_strs(keys)
+    vals, vo = pack_values(values)
+    if len(vo) - 1 != pk.n:
+        raise ValueError("keys and values differ in length")
+    bf_first, bo = plan_blocks(key_offsets(pk), vo, block_size)
+    data = encode_data_blocks(pk, vals, vo, bf_first, bo, dev)
+    meta, metas = meta_blocks(keys, bf_first, bo)
+    bloom = BloomFilter.build_from_keys_and_fp_rate(pk, fp_rate, device=dev)
+    return encode_sstable(memoryview(data), meta, bloom), metas, bloom
