@@ -54,6 +54,9 @@ for step in "$@"; do
               run rh_c4_n2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29514 bench.py --gpus 2 --config c4 --steps 2 --warmup 1
               unset PBF_BENCH_DEVICE PBF_BENCH_BACKEND ;;
     pytest_sst) run pytest_sst 600 python -u -m pytest tests/test_gpu_sstable_data.py -m gpu -x -v -rf --timeout 300 --timeout-method thread ;;
+    bench_sst) run bench_sst 600 python bench.py --config sst --steps 20 --warmup 3
+               run prof_sst 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_sst -o run -- python bench.py --config sst --steps 10 --warmup 2 --cpu-seconds 1
+               python tools/prof_summary.py gpurun_out/prof_sst > gpurun_out/prof_sst_summary.txt 2>&1 ;;
     bench_atomic) run bench_atomic 600 python bench.py --steps 10 --warmup 3 --build-mode 1 --no-cpu-baseline ;;
     bench_tt) run bench_tt 300 python bench.py --steps 20 --warmup 5 --build-mode 2 --probe-mode 2 --no-cpu-baseline --no-host-inclusive ;;
     bench_modes) for bm in 1 2; do for pm in 1 2; do run bench_b${bm}_p${pm} 300 python bench.py --steps 20 --warmup 5 --build-mode $bm --probe-mode $pm --no-cpu-baseline; done; done ;;
