@@ -219,6 +219,8 @@ struct pbf_filter {
     int probe_mode = PBF_PROBE_AUTO;
     int last_probe_mode = 0;
     DevBuf regions, fill, ovf, ovf_count, subcnt, rbits, neg, alive, hw;
+    uint32_t ovf_phase = 0;  // which of the two overflow counters the next build uses
+    bool ovf_init = false;
     DevBuf dkeys, doffs, dout;
     PinBuf pin[2];
     int pin_next = 0;
@@ -416,12 +418,17 @@ int run_tiled(pbf_filter_t* f, const Batch& b) {
     HIP_TRY(f->fill.ensure(size_t(pg.G) * B * 4));
     HIP_TRY(f->ovf.ensure(std::max<uint64_t>(b.n * k, 1) * 4));
     HIP_TRY(f->ovf_count.ensure(64));
+    if (!f->ovf_init) {  // two counters, used alternately; each build's k_ovf_build zeroes the other
+        HIP_TRY(hipMemsetAsync(f->ovf_count.p, 0, 64, f->stream));
+        f->ovf_init = true;
+    }
     auto* regions = static_cast<uint32_t*>(f->regions.p);
     auto* fill = static_cast<uint32_t*>(f->fill.p);
     auto* ovf = static_cast<uint32_t*>(f->ovf.p);
-    auto* ovf_count = static_cast<uint32_t*>(f->ovf_count.p);
+    auto* ovf_count = static_cast<uint32_t*>(f->ovf_count.p) + f->ovf_phase;
+    uint32_t* ovf_next = static_cast<uint32_t*>(f->ovf_count.p) + (f->ovf_phase ^ 1);
+    f->ovf_phase ^= 1;
     hipStream_t s = f->stream;
-    HIP_TRY(hipMemsetAsync(ovf_count, 0, 4, s));
     hipError_t err = hipSuccess;
     dispatch(kmax_for(k), b.km, [&](auto KMAX, auto KM) {
         if constexpr (decltype(KMAX)::value > 0) {  // tiled path only for k <= 32
@@ -432,7 +439,7 @@ int run_tiled(pbf_filter_t* f, const Batch& b) {
                     err = allow_lds(kern, pl.lds_part);
                     if (err == hipSuccess)
                         kern<<<pg.G, kPartThreads, pl.lds_part, s>>>(b.ks, b.n, int(k), tm, pg, regions, fill, nullptr,
-                                                             ovf, ovf_count, ProbeSet{}, 0, nullptr);
+                                                             ovf, ovf_count, ProbeSet{}, 0, nullptr, nullptr);
                 }
             } else {
                 auto kern = k_part<KX, KMD, false>;
@@ -449,7 +456,7 @@ int run_tiled(pbf_filter_t* f, const Batch& b) {
     HIP_TRY(allow_lds(k_tile_build, lds_tile));
     k_tile_build<<<B, 1024, lds_tile, s>>>(tm, pg, regions, fill, f->bitmap, f->pristine ? 1 : 0);
     CHECK_LAUNCH();
-    k_ovf_build<<<256, 256, 0, s>>>(tm, ovf, ovf_count, f->bitmap);
+    k_ovf_build<<<256, 256, 0, s>>>(tm, ovf, ovf_count, f->bitmap, ovf_next);
     CHECK_LAUNCH();
     f->pristine = false;
     return PBF_OK;
@@ -500,7 +507,8 @@ int run_tiled_probe_set(pbf_filter_t* f, pbf_filter_t* const* fs, uint32_t nf, c
     // One probe round: seeds [sbase, sbase + kr) of the keys `alive` marks (all if null), each
     // filter's round hit mask (AND alive) into outs[i] + hm_off.
     auto round = [&](int sbase, uint32_t kr, const uint32_t* alive, uint8_t* const* outs) -> int {
-        HIP_TRY(hipMemsetAsync(neg, 0, neg_bytes * nf, s));
+        // the ring partition zeroes neg (and presets hw for the first filter) itself
+        if (!pg.ring) HIP_TRY(hipMemsetAsync(neg, 0, neg_bytes * nf, s));
         hipError_t err = hipSuccess;
         dispatch(kmax_for(kr), b.km, [&](auto KMAX, auto KM) {
             if constexpr (decltype(KMAX)::value > 0) {
@@ -511,7 +519,8 @@ int run_tiled_probe_set(pbf_filter_t* f, pbf_filter_t* const* fs, uint32_t nf, c
                         err = allow_lds(kern, pl.lds_part);
                         if (err == hipSuccess)
                             kern<<<pg.G, kPartThreads, pl.lds_part, s>>>(b.ks, b.n, int(kr), tm, pg, regions, fill,
-                                                                 subcnt, nullptr, nullptr, ps, sbase, alive);
+                                                                 subcnt, nullptr, nullptr, ps, sbase, alive,
+                                                                 S > 1 ? hw : nullptr);
                     }
                 } else {
                     auto kern = k_part<KX, KMD, true>;
@@ -527,7 +536,7 @@ int run_tiled_probe_set(pbf_filter_t* f, pbf_filter_t* const* fs, uint32_t nf, c
         if (pg.ring) HIP_TRY(allow_lds(k_gather_ring, pl.lds_gather));
         else HIP_TRY(allow_lds(k_gather, pl.lds_gather));
         for (uint32_t i = 0; i < nf; ++i) {
-            if (S > 1) HIP_TRY(hipMemsetAsync(hw, 0xFF, neg_bytes, s));
+            if (S > 1 && (i > 0 || !pg.ring)) HIP_TRY(hipMemsetAsync(hw, 0xFF, neg_bytes, s));
             k_tile_probe<<<B, 1024, lds_tile, s>>>(tm, pg, regions, fill, fs[i]->bitmap, R, expand);
             CHECK_LAUNCH();
             const uint32_t* negi = neg + i * neg_words;

@@ -55,7 +55,8 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
                                                     uint32_t* __restrict__ regions, uint32_t* __restrict__ fill,
                                                     uint32_t* __restrict__ pref, uint32_t* __restrict__ ovf,
                                                     uint32_t* __restrict__ ovf_count,
-                                                    ProbeSet ps, int sbase, const uint32_t* __restrict__ alive) {
+                                                    ProbeSet ps, int sbase, const uint32_t* __restrict__ alive,
+                                                    uint32_t* __restrict__ hw_init) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     const uint32_t B = tm.nbuckets;
     const uint32_t RC = pg.ring, GS = RC / 2, rmask = RC - 1;
@@ -76,6 +77,15 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
     }
     const uint64_t k0 = uint64_t(g) * pg.kpw;
     const uint64_t k1 = min(n, k0 + pg.kpw);
+    if constexpr (PROBE) {
+        // this workgroup's words of every filter's miss bits (neg) start at 0 and, when the
+        // gather is split, of the ANDed gather words (hw_init) at all ones: no memset launches
+        for (uint64_t w = (k0 >> 5) + tid; w < ((k1 + 31) >> 5); w += nt) {
+            for (uint32_t f = 0; f < ps.nf; ++f) ps.neg[f * ps.neg_stride + w] = 0u;
+            if (hw_init) hw_init[w] = ~0u;
+        }
+        __syncthreads();  // before any spill of this workgroup ORs into neg
+    }
     constexpr int P = kRingPrefetch;
     constexpr bool F16 = KM == kFixed16;
     uint4 kw[F16 ? P : 1];

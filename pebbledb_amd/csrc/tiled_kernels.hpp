@@ -419,8 +419,12 @@ __global__ void __launch_bounds__(1024) k_tile_build(TileMap tm, PartGeom pg, co
     store_tile(tile, bitmap, w0, nw);
 }
 
+// `reset`: the other of the handle's two overflow counters (the previous build's), zeroed here
+// for the next build, so no memset launch precedes a build.
 __global__ void __launch_bounds__(256) k_ovf_build(TileMap tm, const uint32_t* __restrict__ ovf,
-                                                   const uint32_t* __restrict__ ovf_count, uint32_t* __restrict__ bitmap) {
+                                                   const uint32_t* __restrict__ ovf_count, uint32_t* __restrict__ bitmap,
+                                                   uint32_t* __restrict__ reset) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) *reset = 0u;
     const uint32_t cnt = *ovf_count;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < cnt; i += gridDim.x * blockDim.x) {
         const uint64_t bit = pos_to_bit(ovf[i], tm);

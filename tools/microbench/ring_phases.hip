@@ -28,12 +28,17 @@ void run(const char* name, uint8_t* keys, uint64_t n, int k, uint32_t* alive) {
     KeySet ks{keys, nullptr, nullptr, 16};
     const size_t lds = size_t((2 * B + 16 * 128 + 3) & ~3u) * 4 + size_t(B) * 32 * 4;
     auto kern = k_part_ring<KMAX, 0, PROBE, true>;
+    ProbeSet ps{};
+    ps.nf = PROBE ? 1 : 0;
+    ps.bm[0] = bitmap;
+    ps.neg = neg;
+    ps.neg_stride = n / 32 + 1;
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipEvent_t a, b; hipEventCreate(&a); hipEventCreate(&b);
-    kern<<<pg.G, 1024, lds>>>(ks, n, k, tm, pg, regions, fill, pref, ovf, cnt, bitmap, neg, PROBE ? 1 : 0, alive);
+    kern<<<pg.G, 1024, lds>>>(ks, n, k, tm, pg, regions, fill, pref, ovf, cnt, ps, PROBE ? 1 : 0, alive, nullptr);
     hipMemset(st, 0, 64 * 8);
     hipEventRecord(a);
-    kern<<<pg.G, 1024, lds>>>(ks, n, k, tm, pg, regions, fill, pref, ovf, cnt, bitmap, neg, PROBE ? 1 : 0, alive);
+    kern<<<pg.G, 1024, lds>>>(ks, n, k, tm, pg, regions, fill, pref, ovf, cnt, ps, PROBE ? 1 : 0, alive, nullptr);
     hipEventRecord(b); hipEventSynchronize(b);
     float ms; hipEventElapsedTime(&ms, a, b);
     std::vector<unsigned long long> h(64);
