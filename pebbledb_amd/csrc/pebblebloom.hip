@@ -323,8 +323,8 @@ uint32_t ring_entries(uint32_t B, uint32_t k, bool probe, uint32_t tb) {
 // Gather LDS = the key bitmap of a partition workgroup + one u16 run-boundary row (`row`
 // entries) per tile of the split.  Splits start at gather_splits() and double (up to 64) while
 // the workgroup does not fit, so large batches stay in one pipeline.
-void set_gather(PartPlan& pl, uint32_t B, uint32_t row) {
-    const size_t kb = size_t((pl.pg.kpw + 31) / 32) * 4;
+void set_gather(PartPlan& pl, uint32_t B, uint32_t row, uint32_t nf = 1) {
+    const size_t kb = size_t((pl.pg.kpw + 31) / 32) * 4 * nf;  // one key bitmap per fused filter
     uint32_t S = gather_splits();
     auto lds = [&](uint32_t sp) { return kb + size_t((B + sp - 1) / sp) * row * 2 + 16; };
     while (lds(S) > 156 * 1024 && S < 64 && S < B) S *= 2;
@@ -332,7 +332,7 @@ void set_gather(PartPlan& pl, uint32_t B, uint32_t row) {
     pl.lds_gather = lds(S);
 }
 
-PartPlan plan_ring(uint32_t B, uint32_t k, uint64_t n, uint32_t rc, double share) {
+PartPlan plan_ring(uint32_t B, uint32_t k, uint64_t n, uint32_t rc, double share, uint32_t nf = 1) {
     PartPlan pl{};
     const uint64_t kps = kRingKeysPerSub;
     const uint64_t G0 = std::min<uint64_t>(256, std::max<uint64_t>(1, (n + kps - 1) / kps));
@@ -348,7 +348,7 @@ PartPlan plan_ring(uint32_t B, uint32_t k, uint64_t n, uint32_t rc, double share
     const uint64_t cap = uint64_t(mu + 8.0 * std::sqrt(mu) + 32.0);
     pl.pg.cap = uint32_t(((cap + 31) / 32) * 32);
     pl.lds_part = size_t((2 * B + 16 * 128 + 3) & ~3u) * 4 + size_t(B) * rc * 4;
-    set_gather(pl, B, pl.pg.nq + 1);
+    set_gather(pl, B, pl.pg.nq + 1, nf);
     return pl;
 }
 
@@ -397,12 +397,13 @@ double busiest_tile_share(const TileMap& tm) {
     return std::min(1.0, max_pre * tile / 4294967296.0);
 }
 
-PartPlan plan_for(const TileMap& tm, uint32_t k, int km, uint64_t n, bool probe) {
+// nf: filters one ring gather serves at once (a multi-filter probe).
+PartPlan plan_for(const TileMap& tm, uint32_t k, int km, uint64_t n, bool probe, uint32_t nf = 1) {
     const uint32_t B = tm.nbuckets;
     const double share = busiest_tile_share(tm);
     const uint32_t rc = ring_entries(B, k, probe, tm.tb);
     if (rc) {
-        const PartPlan pl = plan_ring(B, k, n, rc, share);
+        const PartPlan pl = plan_ring(B, k, n, rc, share, nf);
         if (pl.pg.cap < (1u << 20)) return pl;  // flush descriptors hold a region position in 20 bits
     }
     return plan_partition(B, k, km, n, probe, share);
@@ -471,13 +472,15 @@ int run_tiled_probe_set(pbf_filter_t* f, pbf_filter_t* const* fs, uint32_t nf, c
     const TileMap& tm = f->tm;
     const uint32_t B = tm.nbuckets;
     const uint32_t k = f->k;
-    const PartPlan pl = plan_for(tm, k, b.km, b.n, true);
+    const PartPlan pl = plan_for(tm, k, b.km, b.n, true, nf);
     const PartGeom& pg = pl.pg;
+    const uint32_t nfg = pg.ring ? nf : 1;  // filters per gather launch (R and hw copies)
     HIP_TRY(f->regions.ensure(size_t(pg.G) * B * pg.cap * 4));
     HIP_TRY(f->fill.ensure(size_t(pg.G) * B * 4));
     // sort partition: per-sub-chunk tile counts; ring partition: cumulative counts per 4 sub-chunks
     HIP_TRY(f->subcnt.ensure(pg.ring ? size_t(pg.G) * B * (pg.nq + 1) * 4 : size_t(pg.G) * pg.nsub * B * 4));
-    HIP_TRY(f->rbits.ensure(size_t(pg.G) * B * (pg.cap / 32) * 4));
+    const size_t r_words = size_t(pg.G) * B * (pg.cap / 32);
+    HIP_TRY(f->rbits.ensure(r_words * 4 * nfg));
     const uint64_t neg_words = (b.n + 31) / 32;
     const size_t neg_bytes = neg_words * 4;
     HIP_TRY(f->neg.ensure(neg_bytes * nf));
@@ -489,9 +492,10 @@ int run_tiled_probe_set(pbf_filter_t* f, pbf_filter_t* const* fs, uint32_t nf, c
     hipStream_t s = f->stream;
     // gather split over S tile ranges (several small workgroups per CU)
     const uint32_t S = pl.gsplit;
+    const bool use_hw = S > 1 || nfg > 1;
     uint32_t* hw = nullptr;
-    if (S > 1) {
-        HIP_TRY(f->hw.ensure(neg_bytes));
+    if (use_hw) {
+        HIP_TRY(f->hw.ensure(neg_bytes * nfg));
         hw = static_cast<uint32_t*>(f->hw.p);
     }
     ProbeSet ps{};
@@ -520,7 +524,7 @@ int run_tiled_probe_set(pbf_filter_t* f, pbf_filter_t* const* fs, uint32_t nf, c
                         if (err == hipSuccess)
                             kern<<<pg.G, kPartThreads, pl.lds_part, s>>>(b.ks, b.n, int(kr), tm, pg, regions, fill,
                                                                  subcnt, nullptr, nullptr, ps, sbase, alive,
-                                                                 S > 1 ? hw : nullptr);
+                                                                 use_hw ? hw : nullptr);
                     }
                 } else {
                     auto kern = k_part<KX, KMD, true>;
@@ -533,19 +537,34 @@ int run_tiled_probe_set(pbf_filter_t* f, pbf_filter_t* const* fs, uint32_t nf, c
         });
         HIP_TRY(err);
         CHECK_LAUNCH();
-        if (pg.ring) HIP_TRY(allow_lds(k_gather_ring, pl.lds_gather));
+        auto gring = nf > 1 ? k_gather_ring<kMaxProbeSet> : k_gather_ring<1>;
+        if (pg.ring) HIP_TRY(allow_lds(gring, pl.lds_gather));
         else HIP_TRY(allow_lds(k_gather, pl.lds_gather));
+        const dim3 grid(pg.G, S);
+        if (pg.ring) {
+            // every filter's tile test, then ONE gather over the shared region entries
+            for (uint32_t i = 0; i < nf; ++i) {
+                k_tile_probe<<<B, 1024, lds_tile, s>>>(tm, pg, regions, fill, fs[i]->bitmap, R + i * r_words, expand);
+                CHECK_LAUNCH();
+            }
+            gring<<<grid, 512, pl.lds_gather, s>>>(tm, pg, b.n, regions, R, fill, subcnt, neg, alive, outs[0] + hm_off,
+                                                  hw, nf, r_words, neg_words);
+            CHECK_LAUNCH();
+            if (use_hw) {
+                for (uint32_t i = 0; i < nf; ++i) {
+                    k_hw_to_hitmask<<<grid_for(neg_words, 256, 4096), 256, 0, s>>>(hw + i * neg_words, b.n,
+                                                                                   outs[i] + hm_off);
+                    CHECK_LAUNCH();
+                }
+            }
+            return PBF_OK;
+        }
         for (uint32_t i = 0; i < nf; ++i) {
-            if (S > 1 && (i > 0 || !pg.ring)) HIP_TRY(hipMemsetAsync(hw, 0xFF, neg_bytes, s));
+            if (S > 1) HIP_TRY(hipMemsetAsync(hw, 0xFF, neg_bytes, s));
             k_tile_probe<<<B, 1024, lds_tile, s>>>(tm, pg, regions, fill, fs[i]->bitmap, R, expand);
             CHECK_LAUNCH();
-            const uint32_t* negi = neg + i * neg_words;
-            const dim3 grid(pg.G, S);
-            if (pg.ring)
-                k_gather_ring<<<grid, 512, pl.lds_gather, s>>>(tm, pg, b.n, regions, R, fill, subcnt, negi, alive,
-                                                              outs[i] + hm_off, hw);
-            else
-                k_gather<<<grid, 512, pl.lds_gather, s>>>(tm, pg, b.n, regions, R, subcnt, negi, outs[i] + hm_off, hw);
+            k_gather<<<grid, 512, pl.lds_gather, s>>>(tm, pg, b.n, regions, R, subcnt, neg + i * neg_words,
+                                                      outs[i] + hm_off, hw);
             CHECK_LAUNCH();
             if (S > 1) {
                 k_hw_to_hitmask<<<grid_for(neg_words, 256, 4096), 256, 0, s>>>(hw, b.n, outs[i] + hm_off);
@@ -602,11 +621,11 @@ bool want_tiled_probe(pbf_filter_t* f, uint64_t n) {
 
 // Largest probe batch one tiled pipeline takes: k_gather keeps a u16 run-boundary table
 // (B x (nsub+1)) and a bit per key of its workgroup in LDS, and positions stay u32.
-uint64_t tiled_probe_batch(pbf_filter_t* f, int km) {
+uint64_t tiled_probe_batch(pbf_filter_t* f, int km, uint32_t nf = 1) {
     const uint32_t k = f->k;
     uint64_t n = std::max<uint64_t>(64, (kMaxPositions / k) & ~uint64_t(63));
     for (;;) {
-        const PartPlan pl = plan_for(f->tm, k, km, n, true);
+        const PartPlan pl = plan_for(f->tm, k, km, n, true, nf);
         if ((pl.lds_gather <= 156 * 1024 && pl.pg.cap <= 65535) || n <= 64 * 1024) return n;
         n = std::max<uint64_t>(64 * 1024, (n / 2) & ~uint64_t(63));
     }
@@ -702,7 +721,7 @@ int probe_multi_device(pbf_filter_t* const* fs, uint32_t nf, const Batch& b, uin
             HIP_TRY(hipEventRecord(fs[i]->ev, fs[i]->stream));
             HIP_TRY(hipStreamWaitEvent(s0, fs[i]->ev, 0));
         }
-        const uint64_t per = tiled_probe_batch(f0, b.km);
+        const uint64_t per = tiled_probe_batch(f0, b.km, std::min<uint32_t>(nf, kMaxProbeSet));
         for (uint64_t i0 = 0; i0 < b.n; i0 += per) {
             Batch c = b;
             c.n = std::min<uint64_t>(per, b.n - i0);

@@ -79,10 +79,12 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
     const uint64_t k1 = min(n, k0 + pg.kpw);
     if constexpr (PROBE) {
         // this workgroup's words of every filter's miss bits (neg) start at 0 and, when the
-        // gather is split, of the ANDed gather words (hw_init) at all ones: no memset launches
+        // gather ANDs into words, every filter's gather words (hw_init) at all ones: no memsets
         for (uint64_t w = (k0 >> 5) + tid; w < ((k1 + 31) >> 5); w += nt) {
-            for (uint32_t f = 0; f < ps.nf; ++f) ps.neg[f * ps.neg_stride + w] = 0u;
-            if (hw_init) hw_init[w] = ~0u;
+            for (uint32_t f = 0; f < ps.nf; ++f) {
+                ps.neg[f * ps.neg_stride + w] = 0u;
+                if (hw_init) hw_init[f * ps.neg_stride + w] = ~0u;
+            }
         }
         __syncthreads();  // before any spill of this workgroup ORs into neg
     }
@@ -253,21 +255,27 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
 
 // Probe gather for the ring partition: workgroup (g, sp) owns the keys [g*kpw, (g+1)*kpw) of
 // partition workgroup g and the tiles [sp*B/S, (sp+1)*B/S) of its regions (S = gridDim.y
-// splits, so the gather runs several small workgroups per CU instead of one large one).
-// Entries of sub-chunks 4q..4q+3 lie in [pref[q], pref[q+1]) of their region, so a failed entry
-// at position r belongs to sub-chunk 4q + (entry >> 30) with q the last group whose
-// pref[q] <= r; its key is that sub-chunk's first key + the entry's slot.  A failed entry clears
-// its key's bit in an LDS bitmap of the workgroup's keys.  S = 1 writes the hit-mask words
-// directly; S > 1 ANDs them into `hw` (one u32 per 32 keys, preset to all ones) and
-// k_hw_to_hitmask writes the hit mask.
-//   LDS: kbits[kpw/32], pref rows of the split's tiles as u16 ((B/S) x (nq+1)).
+// splits, so the gather runs several small workgroups per CU instead of one large one), for nf
+// filters at once (a multi-filter probe: the region entries are read once, each filter's
+// result bits R + f * r_stride).  Entries of sub-chunks 4q..4q+3 lie in [pref[q], pref[q+1]) of
+// their region, so a failed entry at position r belongs to sub-chunk 4q + (entry >> 30) with q
+// the last group whose pref[q] <= r; its key is that sub-chunk's first key + the entry's slot.
+// A failed entry clears its key's bit in the filter's LDS bitmap of the workgroup's keys.
+// S = 1 and nf = 1 writes the hit-mask words directly; otherwise the words are ANDed into
+// hw + f * neg_stride (one u32 per 32 keys, preset to all ones) and k_hw_to_hitmask writes
+// each filter's hit mask.
+//   LDS: nf x kbits[kpw/32], pref rows of the split's tiles as u16 ((B/S) x (nq+1)).
+// NFM: compile-time bound on nf (1 for a single filter: no per-filter registers or loops).
+template <int NFM>
 __global__ void __launch_bounds__(512) k_gather_ring(TileMap tm, PartGeom pg, uint64_t n,
                                                      const uint32_t* __restrict__ regions,
                                                      const uint32_t* __restrict__ R, const uint32_t* __restrict__ fill,
                                                      const uint32_t* __restrict__ pref,
                                                      const uint32_t* __restrict__ neg, const uint32_t* __restrict__ alive,
-                                                     uint8_t* __restrict__ hitmask, uint32_t* __restrict__ hw) {
+                                                     uint8_t* __restrict__ hitmask, uint32_t* __restrict__ hw,
+                                                     uint32_t nf, uint64_t r_stride, uint64_t neg_stride) {
     extern __shared__ uint32_t smem[];
+    if constexpr (NFM == 1) nf = 1;
     const uint32_t B = tm.nbuckets, cap = pg.cap, wpr = cap / 32, nqs = pg.nq + 1;
     const uint32_t tid = threadIdx.x, nt = blockDim.x;
     const uint32_t lane = tid & 63, wave = tid >> 6, nwaves = nt >> 6;
@@ -279,21 +287,23 @@ __global__ void __launch_bounds__(512) k_gather_ring(TileMap tm, PartGeom pg, ui
     const uint64_t k1 = min(n, k0 + pg.kpw);
     const uint32_t nkeys = uint32_t(k1 - k0);
     const uint32_t kw = uint32_t((pg.kpw + 31) / 32);
-    uint32_t* kbits = smem;                                    // kw words
-    uint16_t* lpref = reinterpret_cast<uint16_t*>(kbits + kw);  // nb * nqs (values <= cap < 2^16)
+    uint32_t* kbits = smem;                                         // nf x kw words
+    uint16_t* lpref = reinterpret_cast<uint16_t*>(kbits + nf * kw);  // nb * nqs (values <= cap < 2^16)
     const uint32_t* gp = pref + uint64_t(g) * nqs * B;  // [q][b] in memory, [b][q] in LDS
     for (uint32_t x = tid; x < nb * nqs; x += nt) {
         const uint32_t q = x / nb, bb = x - q * nb;
         lpref[bb * nqs + q] = uint16_t(gp[uint64_t(q) * B + b_lo + bb]);
     }
-    for (uint32_t w = tid; w < kw; w += nt) {
-        const uint32_t key0 = w * 32;
-        uint32_t m = key0 >= nkeys ? 0u : (nkeys - key0 >= 32 ? ~0u : ((1u << (nkeys - key0)) - 1u));
-        if (m) {  // k0 is a multiple of 64
-            m &= ~neg[(k0 + key0) >> 5];
-            if (alive) m &= alive[(k0 + key0) >> 5];  // refuted by an earlier probe round
+    for (uint32_t f = 0; f < nf; ++f) {
+        for (uint32_t w = tid; w < kw; w += nt) {
+            const uint32_t key0 = w * 32;
+            uint32_t m = key0 >= nkeys ? 0u : (nkeys - key0 >= 32 ? ~0u : ((1u << (nkeys - key0)) - 1u));
+            if (m) {  // k0 is a multiple of 64
+                m &= ~neg[f * neg_stride + ((k0 + key0) >> 5)];
+                if (alive) m &= alive[(k0 + key0) >> 5];  // refuted by an earlier probe round
+            }
+            kbits[f * kw + w] = m;
         }
-        kbits[w] = m;
     }
     lds_barrier();
     constexpr int U = 4;
@@ -307,23 +317,30 @@ __global__ void __launch_bounds__(512) k_gather_ring(TileMap tm, PartGeom pg, ui
         for (int u = 0; u < U; ++u) maxf = max(maxf, fillb[u]);
         for (uint32_t r0 = 0; r0 < maxf; r0 += 256) {
             uint4 v[U];
-            uint32_t rw[U];
+            uint32_t rw[NFM][U];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const uint32_t b = min(b0 + u * nwaves, b_hi - 1);
                 const uint32_t r = min(r0 + lane * 4, (max(fillb[u], 1u) - 1) & ~3u);
                 const uint64_t reg = region_id(g, b, pg.G, B);
                 v[u] = *reinterpret_cast<const uint4*>(regions + reg * cap + r);
-                rw[u] = R[reg * wpr + (r >> 5)];
+#pragma unroll
+                for (int f = 0; f < NFM; ++f)
+                    if (uint32_t(f) < nf) rw[f][u] = R[f * r_stride + reg * wpr + (r >> 5)];
             }
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const uint32_t b = b0 + u * nwaves;
                 const uint32_t r = r0 + lane * 4;
                 if (b < b_hi && r < fillb[u]) {
-                    uint32_t fails = ~r_quad(rw[u], r) & 0xFu;
-                    if (fillb[u] - r < 4) fails &= (1u << (fillb[u] - r)) - 1u;
-                    if (fails) {
+                    const uint32_t lim = fillb[u] - r < 4 ? (1u << (fillb[u] - r)) - 1u : 0xFu;
+                    uint32_t fl[NFM], any = 0;
+#pragma unroll
+                    for (int f = 0; f < NFM; ++f) {
+                        fl[f] = uint32_t(f) < nf ? (~r_quad(rw[f][u], r) & lim) : 0u;
+                        any |= fl[f];
+                    }
+                    if (any) {
                         // q = the last group with pref[q] <= r (pref non-decreasing, pref[0] = 0);
                         // a fixed-trip binary search keeps the wave's lanes together
                         const uint16_t* pb = lpref + (b - b_lo) * nqs;
@@ -336,11 +353,13 @@ __global__ void __launch_bounds__(512) k_gather_ring(TileMap tm, PartGeom pg, ui
                         const uint32_t vv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
 #pragma unroll
                         for (int t = 0; t < 4; ++t) {
-                            if ((fails >> t) & 1u) {
+                            if ((any >> t) & 1u) {
                                 while (lo + 1 < nqs && pb[lo + 1] <= r + t) ++lo;
                                 const uint32_t jj = lo * 4 + (vv[t] >> 30);
                                 const uint32_t key = jj * kRingKeysPerSub + ((vv[t] >> kSlotShift) & 1023u);
-                                atomicAnd(kbits + (key >> 5), ~(1u << (key & 31)));
+#pragma unroll
+                                for (int f = 0; f < NFM; ++f)
+                                    if ((fl[f] >> t) & 1u) atomicAnd(kbits + f * kw + (key >> 5), ~(1u << (key & 31)));
                             }
                         }
                     }
@@ -349,8 +368,9 @@ __global__ void __launch_bounds__(512) k_gather_ring(TileMap tm, PartGeom pg, ui
         }
     }
     lds_barrier();
-    if (S > 1) {
-        for (uint32_t w = tid; w * 32 < nkeys; w += nt) atomicAnd(hw + (k0 >> 5) + w, kbits[w]);
+    if (S > 1 || nf > 1) {
+        for (uint32_t f = 0; f < nf; ++f)
+            for (uint32_t w = tid; w * 32 < nkeys; w += nt) atomicAnd(hw + f * neg_stride + (k0 >> 5) + w, kbits[f * kw + w]);
         return;
     }
     for (uint32_t w = tid; w * 32 < nkeys; w += nt) {

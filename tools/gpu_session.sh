@@ -57,6 +57,8 @@ for step in "$@"; do
     bench_sst) run bench_sst 600 python bench.py --config sst --steps 20 --warmup 3
                run prof_sst 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_sst -o run -- python bench.py --config sst --steps 10 --warmup 2 --cpu-seconds 1
                python tools/prof_summary.py gpurun_out/prof_sst > gpurun_out/prof_sst_summary.txt 2>&1 ;;
+    prof_c5) run prof_c5 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_c5 -o run -- python bench.py --config c5 --steps 3 --warmup 1
+             python tools/prof_summary.py gpurun_out/prof_c5 > gpurun_out/prof_c5_summary.txt 2>&1 ;;
     bench_atomic) run bench_atomic 600 python bench.py --steps 10 --warmup 3 --build-mode 1 --no-cpu-baseline ;;
     bench_tt) run bench_tt 300 python bench.py --steps 20 --warmup 5 --build-mode 2 --probe-mode 2 --no-cpu-baseline --no-host-inclusive ;;
     bench_modes) for bm in 1 2; do for pm in 1 2; do run bench_b${bm}_p${pm} 300 python bench.py --steps 20 --warmup 5 --build-mode $bm --probe-mode $pm --no-cpu-baseline; done; done ;;
@@ -70,6 +72,7 @@ for step in "$@"; do
     traffic) run pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_fetch -o run -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-host-inclusive ${PBF_BENCH_ARGS:-}
              run pmc_write 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_write -o run -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-host-inclusive ${PBF_BENCH_ARGS:-} ;;
     micro) run micro 300 tools/microbench/lds_rates ;;
+    variants2) for r in 1 2; do for v in build/variants/*.so; do nm=$(basename $v .so); PBF_LIB=$PWD/$v run var_${nm}_$r 300 python bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-host-inclusive; done; done ;;
     variants) for v in build/variants/*.so; do nm=$(basename $v .so); PBF_LIB=$PWD/$v run var_$nm 300 python bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-host-inclusive; done
               run var_default 300 python bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-host-inclusive ;;
     rphases) run rphases 300 tools/microbench/ring_phases ;;
