@@ -49,7 +49,8 @@ def pass_of(kernel: str) -> str | None:
         return "probe" if args[2].strip() == "true" else "build"
     if kernel in ("pbf::k_tile_build", "pbf::k_ovf_build"):
         return "build"
-    if kernel in ("pbf::k_tile_probe", "pbf::k_gather", "pbf::k_gather_ring", "pbf::k_hw_to_hitmask"):
+    # templated kernels (k_gather_ring<NF>) match on the name before the argument list
+    if kernel.split("<")[0] in ("pbf::k_tile_probe", "pbf::k_gather", "pbf::k_gather_ring", "pbf::k_hw_to_hitmask"):
         return "probe"
     return None
 
