@@ -1,0 +1,38 @@
+"""tools/traffic_summary.py assigns every kernel of the tiled build/probe passes to its pass, so
+bench.py's roofline.traffic sums the whole pass (a templated name such as k_gather_ring<1> was
+once dropped silently)."""
+import csv
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "tools"))
+
+from traffic_summary import pass_of  # noqa: E402
+
+# kernels that belong to no timed pass of the C2 step (key generation, direct paths, encoder)
+NOT_IN_A_PASS = ("k_gen_", "k_popcount", "k_probe", "k_build_atomic", "k_encode_blocks", "k_hash")
+
+
+def test_pass_of_names():
+    assert pass_of("pbf::k_part_ring<8, 0, true, true>") == "probe"
+    assert pass_of("pbf::k_part_ring<8, 0, false, true>") == "build"
+    assert pass_of("pbf::k_part<8, 1, true>") == "probe"
+    assert pass_of("pbf::k_tile_build") == "build"
+    assert pass_of("pbf::k_ovf_build") == "build"
+    assert pass_of("pbf::k_tile_probe") == "probe"
+    assert pass_of("pbf::k_gather_ring<1>") == "probe"
+    assert pass_of("pbf::k_gather_ring<8>") == "probe"
+    assert pass_of("pbf::k_hw_to_hitmask") == "probe"
+    assert pass_of("__amd_rocclr_copyBuffer") is None
+
+
+def test_every_profiled_pass_kernel_is_assigned():
+    path = os.path.join(REPO, "profiles", "r01", "s8", "kernel_stats.csv")
+    names = [r["Name"].split("(")[0].replace("void ", "").strip() for r in csv.DictReader(open(path))]
+    pbf = [n for n in names if n.startswith("pbf::")]
+    assert pbf
+    for n in pbf:
+        if any(n.split("::")[1].startswith(p) for p in NOT_IN_A_PASS):
+            continue
+        assert pass_of(n) in ("build", "probe"), n
