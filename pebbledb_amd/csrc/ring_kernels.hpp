@@ -204,7 +204,7 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
                         const uint32_t tb = d & 0xFFFu;
                         const uint32_t e = (d >> 12) + q * 4;  // region position
                         const uint4 v = *reinterpret_cast<const uint4*>(ring + tb * RC + (e & rmask));
-                        *reinterpret_cast<uint4*>(regions + region_id(g, tb, pg.G, B) * cap + e) = v;
+                        st_stream<(PBF_NT_STORE & (PROBE ? 2 : 1)) != 0>(regions + region_id(g, tb, pg.G, B) * cap + e, v);
                     }
                 }
                 __builtin_amdgcn_wave_barrier();
@@ -238,7 +238,7 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
                     const uint32_t tb = d & 0xFFFu;
                     const uint32_t e = (d >> 12) + q * 4;
                     const uint4 v = *reinterpret_cast<const uint4*>(ring + tb * RC + (e & rmask));
-                    *reinterpret_cast<uint4*>(regions + region_id(g, tb, pg.G, B) * cap + e) = v;
+                    st_stream<(PBF_NT_STORE & (PROBE ? 2 : 1)) != 0>(regions + region_id(g, tb, pg.G, B) * cap + e, v);
                 }
             }
             __builtin_amdgcn_wave_barrier();
@@ -323,7 +323,7 @@ __global__ void __launch_bounds__(512) k_gather_ring(TileMap tm, PartGeom pg, ui
                 const uint32_t b = min(b0 + u * nwaves, b_hi - 1);
                 const uint32_t r = min(r0 + lane * 4, (max(fillb[u], 1u) - 1) & ~3u);
                 const uint64_t reg = region_id(g, b, pg.G, B);
-                v[u] = *reinterpret_cast<const uint4*>(regions + reg * cap + r);
+                v[u] = ld_stream(regions + reg * cap + r);
 #pragma unroll
                 for (int f = 0; f < NFM; ++f)
                     if (uint32_t(f) < nf) rw[f][u] = R[f * r_stride + reg * wpr + (r >> 5)];

@@ -34,6 +34,39 @@
 
 namespace pbf {
 
+// Streaming access to the region entries and the bitmap tile write-out: each byte is written
+// once and read back once or twice by a later kernel, far beyond L2. PBF_NT_LOAD marks the
+// region-entry loads non-temporal; PBF_NT_STORE is a bit set — 1: build partition stores,
+// 2: probe partition stores, 4: k_tile_build's bitmap write-out. Defaults = the best of the A/B
+// builds on C2 (profiles/r01/s9/nt_ab.txt): loads + probe partition + bitmap write-out
+// (0.886 -> 0.822 ms/step); non-temporal build-partition stores measured slower (+10 us).
+#ifndef PBF_NT_STORE
+#define PBF_NT_STORE 6
+#endif
+#ifndef PBF_NT_LOAD
+#define PBF_NT_LOAD 1
+#endif
+typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+
+template <bool NT>
+__device__ __forceinline__ void st_stream(uint32_t* p, uint4 v) {
+    if constexpr (NT) {
+        const u32x4v x = {v.x, v.y, v.z, v.w};
+        __builtin_nontemporal_store(x, reinterpret_cast<u32x4v*>(p));
+    } else {
+        *reinterpret_cast<uint4*>(p) = v;
+    }
+}
+
+__device__ __forceinline__ uint4 ld_stream(const uint32_t* p) {
+#if PBF_NT_LOAD
+    const u32x4v x = __builtin_nontemporal_load(reinterpret_cast<const u32x4v*>(p));
+    return make_uint4(x.x, x.y, x.z, x.w);
+#else
+    return *reinterpret_cast<const uint4*>(p);
+#endif
+}
+
 struct TileMap {
     IndexMap im;
     uint32_t tb;           // log2 positions per tile (<= 20)
@@ -346,7 +379,7 @@ __device__ __forceinline__ void store_tile(const uint32_t* tile, uint32_t* __res
     const uint32_t tid = threadIdx.x, nt = blockDim.x;
     if ((w0 & 3) == 0 && (nw & 3) == 0) {
         uint4* dst = reinterpret_cast<uint4*>(bitmap + w0);
-        for (uint32_t q = tid; q < nw / 4; q += nt) dst[q] = reinterpret_cast<const uint4*>(tile)[q];
+        for (uint32_t q = tid; q < nw / 4; q += nt) st_stream<(PBF_NT_STORE & 4) != 0>(reinterpret_cast<uint32_t*>(dst + q), reinterpret_cast<const uint4*>(tile)[q]);
     } else {
         for (uint32_t w = tid; w < nw; w += nt) bitmap[w0 + w] = tile[w];
     }
@@ -400,7 +433,7 @@ __global__ void __launch_bounds__(1024) k_tile_build(TileMap tm, PartGeom pg, co
             f[u] = q < G ? fills[q] : 0u;
             // unconditional loads, clamped to the filled part (idle lanes re-read its last line)
             const uint32_t lc = min(lane, (max(f[u], 1u) - 1) >> 2);
-            v[u] = reinterpret_cast<const uint4*>(regions + region_id(min(q, G - 1), b, G, B) * cap)[lc];
+            v[u] = ld_stream(regions + region_id(min(q, G - 1), b, G, B) * cap + lc * 4);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u)
@@ -411,7 +444,7 @@ __global__ void __launch_bounds__(1024) k_tile_build(TileMap tm, PartGeom pg, co
         for (uint32_t q = wave; q < G; q += nwaves) {
             const uint32_t fq = fills[q];
             for (uint32_t c = 64 + lane; c * 4 < fq; c += 64)
-                or_bits4(tile, reinterpret_cast<const uint4*>(regions + region_id(q, b, G, B) * cap)[c], c * 4, fq,
+                or_bits4(tile, ld_stream(regions + region_id(q, b, G, B) * cap + c * 4), c * 4, fq,
                          lmask);
         }
     }
@@ -488,7 +521,7 @@ __global__ void __launch_bounds__(1024) k_tile_probe(TileMap tm, PartGeom pg, co
             const uint32_t c = min(c0 + u * stride + wsub, total - 1);  // unconditional loads
             qq[u] = expand ? uint32_t(wq[c]) : bucket_of(wpre, G, c);
             word[u] = c - wpre[qq[u]];
-            v[u] = reinterpret_cast<const uint4*>(regions + region_id(qq[u], b, G, B) * cap + word[u] * 32)[l];
+            v[u] = ld_stream(regions + region_id(qq[u], b, G, B) * cap + word[u] * 32 + l * 4);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -588,7 +621,7 @@ __global__ void __launch_bounds__(512) k_gather(TileMap tm, PartGeom pg, uint64_
                 const uint32_t b = min(b0 + u * nwaves, b_hi - 1);
                 const uint32_t r = min(r0 + lane * 4, (max(fillb[u], 1u) - 1) & ~3u);
                 const uint64_t reg = region_id(g, b, pg.G, B);
-                v[u] = *reinterpret_cast<const uint4*>(regions + reg * cap + r);
+                v[u] = ld_stream(regions + reg * cap + r);
                 rw[u] = R[reg * wpr + (r >> 5)];
             }
 #pragma unroll
