@@ -97,7 +97,7 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
         for (int u = 0; u < P; ++u) {
             const uint64_t i = c0 + uint64_t(u) * kRingKeysPerSub + tid;
             aw[u] = (alive && i < k1) ? alive[i >> 5] : ~0u;
-            if constexpr (F16) kw[u] = reinterpret_cast<const uint4*>(ks.data)[min(i, n - 1)];
+            if constexpr (F16) kw[u] = ld_stream_nt<PBF_NT_KEYS != 0>(reinterpret_cast<const uint32_t*>(ks.data) + min(i, n - 1) * 4);
         }
     };
     load_batch(k0);

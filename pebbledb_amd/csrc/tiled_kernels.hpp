@@ -58,14 +58,27 @@ __device__ __forceinline__ void st_stream(uint32_t* p, uint4 v) {
     }
 }
 
-__device__ __forceinline__ uint4 ld_stream(const uint32_t* p) {
-#if PBF_NT_LOAD
-    const u32x4v x = __builtin_nontemporal_load(reinterpret_cast<const u32x4v*>(p));
-    return make_uint4(x.x, x.y, x.z, x.w);
-#else
-    return *reinterpret_cast<const uint4*>(p);
-#endif
+template <bool NT>
+__device__ __forceinline__ uint4 ld_stream_nt(const uint32_t* p) {
+    if constexpr (NT) {
+        const u32x4v x = __builtin_nontemporal_load(reinterpret_cast<const u32x4v*>(p));
+        return make_uint4(x.x, x.y, x.z, x.w);
+    } else {
+        return *reinterpret_cast<const uint4*>(p);
+    }
 }
+
+// The partition's 16-B key loads (each key is read once per pass): non-temporal, 0.819 ->
+// 0.801 ms/step on C2. The tile passes' bitmap loads (PBF_NT_TILE) measured no gain: off.
+// A/B records: profiles/r01/s10/nt_ab.txt.
+#ifndef PBF_NT_KEYS
+#define PBF_NT_KEYS 1
+#endif
+#ifndef PBF_NT_TILE
+#define PBF_NT_TILE 0
+#endif
+
+__device__ __forceinline__ uint4 ld_stream(const uint32_t* p) { return ld_stream_nt<PBF_NT_LOAD != 0>(p); }
 
 struct TileMap {
     IndexMap im;
@@ -252,7 +265,7 @@ __global__ void __launch_bounds__(kPartThreads) k_part(KeySet ks, uint64_t n, in
 #pragma unroll
             for (int u = 0; u < KPT; ++u) {
                 const uint64_t i = min(s0 + u * nt + tid, n - 1);
-                kw[u] = reinterpret_cast<const uint4*>(ks.data)[i];
+                kw[u] = ld_stream_nt<PBF_NT_KEYS != 0>(reinterpret_cast<const uint32_t*>(ks.data) + i * 4);
             }
         }
     };
@@ -364,7 +377,7 @@ __device__ __forceinline__ void load_tile(uint32_t* tile, const uint32_t* __rest
         for (uint32_t q0 = tid; q0 < W4; q0 += nt * 8) {
             uint4 v[8];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) v[u] = src[min(q0 + u * nt, W4 - 1)];
+            for (int u = 0; u < 8; ++u) v[u] = ld_stream_nt<PBF_NT_TILE != 0>(reinterpret_cast<const uint32_t*>(src + min(q0 + u * nt, W4 - 1)));
 #pragma unroll
             for (int u = 0; u < 8; ++u)
                 if (q0 + u * nt < W4) reinterpret_cast<uint4*>(tile)[q0 + u * nt] = v[u];
