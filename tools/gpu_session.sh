@@ -75,7 +75,8 @@ for step in "$@"; do
     variants2) for r in 1 2; do for v in build/variants/*.so; do nm=$(basename $v .so); PBF_LIB=$PWD/$v run var_${nm}_$r 300 python bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-host-inclusive; done; done ;;
     variants) for v in build/variants/*.so; do nm=$(basename $v .so); PBF_LIB=$PWD/$v run var_$nm 300 python bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-host-inclusive; done
               run var_default 300 python bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-host-inclusive ;;
-    rphases) run rphases 300 tools/microbench/ring_phases ;;
+    variants_c3) for r in 1 2; do for v in build/variants/*.so; do nm=$(basename $v .so); PBF_LIB=$PWD/$v run c3var_${nm}_$r 300 python bench.py --config c3 --steps 5 --warmup 2 --no-cpu-baseline --no-host-inclusive; done; done ;;
+    rphases)run rphases 300 tools/microbench/ring_phases ;;
     phases) run phases_t0 300 tools/microbench/part_phases 0
             run phases_t16 300 tools/microbench/part_phases 16 ;;
     gapdiag) run native0 120 tools/microbench/pipeline_bench 50 0
