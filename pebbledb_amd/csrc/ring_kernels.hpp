@@ -35,8 +35,9 @@
 namespace pbf {
 
 constexpr uint32_t kRingKeysPerSub = 1024;  // = threads; slot field is 10 bits
+// 2 measured best with the non-temporal streams (C2 A/B over 1/2/3/4/8: profiles/r01/s11/ab.txt)
 #ifndef PBF_RING_PREFETCH
-#define PBF_RING_PREFETCH 4
+#define PBF_RING_PREFETCH 2
 #endif
 constexpr int kRingPrefetch = PBF_RING_PREFETCH;  // sub-chunks of keys loaded per batch
 
