@@ -28,7 +28,7 @@ def test_pass_of_names():
 
 
 def test_every_profiled_pass_kernel_is_assigned():
-    path = os.path.join(REPO, "profiles", "r01", "s10", "kernel_stats.csv")
+    path = os.path.join(REPO, "profiles", "r01", "s12", "kernel_stats.csv")
     names = [r["Name"].split("(")[0].replace("void ", "").strip() for r in csv.DictReader(open(path))]
     pbf = [n for n in names if n.startswith("pbf::")]
     assert pbf
