@@ -1,6 +1,12 @@
 """Benchmark: device-resident bloom build + probe (BASELINE.json metric), one process per GPU.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c1|c3] [--no-cpu-baseline]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c1|c3|c4|c5|sst] [--no-cpu-baseline]
+
+With --gpus N > 1 and no WORLD_SIZE in the environment, bench.py starts the N ranks itself (one
+child process per GPU, RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* set, 127.0.0.1 rendezvous) before
+anything touches a GPU, and exits with the worst child exit code; under torch.distributed.run
+it is one of the ranks.  WORLD_SIZE != --gpus is an error.  --dry-run exercises only that
+launcher and the rendezvous / barrier / max-over-ranks plumbing (gloo, no GPU, no numbers).
 
 Config c2 (default, BASELINE.json configs[1]): per GPU one SSTable filter of m = 2^30 bits
 (nb_bytes = 128 MiB), k = 6, built from 10M 16-byte keys, then probed with 20M keys (the 10M
@@ -52,6 +58,9 @@ def parse():
     ap.add_argument("--no-host-inclusive", action="store_true", help="skip the pinned host<->device leg")
     ap.add_argument("--sync-each-step", action="store_true", help="diagnostic: synchronise after every step")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the bounded CPU sample")
+    ap.add_argument("--no-host-c5", action="store_true", help="c5: skip the host-resident (pinned H2D) leg")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher / rendezvous check only (gloo, no GPU work, no measurement)")
     return ap.parse_args()
 
 
@@ -181,6 +190,67 @@ def all_reduce_scalar(torch, dist, value, op, dtype):
     return t.item()
 
 
+def c5_host_resident(args, filters, mine, hms, q, nq, k, torch, np, L, reps=2):
+    """BASELINE configs[4] as LsmStorage.get batching would run it (src/lsm_storage.py:164-179):
+    the probe batch starts in (pinned) host memory, every GPU copies its own replica in
+    (per-GPU H2D, pbf_probe_multi with keys_on_device = 0: 256 MiB pinned chunks), probes its
+    filters and the hit masks return to host memory.  Rate = key x filter probes / wall time."""
+    import ctypes
+    from pebbledb_amd import _native
+    hq = q.cpu().pin_memory()
+    outs_np = [np.zeros((nq + 7) // 8, dtype=np.uint8) for _ in mine]
+    hs = (ctypes.c_void_p * len(mine))(*[filters[g].handle.value for g in mine])
+    outs = (ctypes.c_void_p * len(mine))(*[a.ctypes.data for a in outs_np])
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        _native.check(L.pbf_probe_multi_fixed(hs, len(mine), ctypes.c_void_p(hq.data_ptr()), 16, nq, outs, 0),
+                      "probe_multi host")
+        ts.append(time.perf_counter() - t0)
+    t = min(ts)
+    same = all(np.array_equal(outs_np[i], hms[g].cpu().numpy()) for i, g in enumerate(mine))
+    return {"ms": round(t * 1e3, 2), "Mprobes_s": round(nq * len(mine) / t / 1e6, 1),
+            "h2d_GBs": round(nq * 16 / t / 1e9, 2), "equal_to_device_resident": bool(same),
+            "what": f"pinned host batch of {nq} 16-B keys -> per-GPU H2D (256 MiB chunks) -> multi-filter probe of "
+                    f"the rank's {len(mine)} filters -> D2H hit masks; best of {reps}"}
+
+
+def c5_cpu_baseline(args, filters, mine, hms, q, n_f, nb_bytes, k, np):
+    """C5's CPU baseline (rank 0, N = 1): the reference algorithm (BigIntBloomPort, Python
+    big-int bitmap) probing filter 0 at full size on a bounded sample, plus the C oracle
+    (OpenMP) probing a 1M-key sample against filter 0 — whose result must equal the GPU's."""
+    from oracle.oracle import BigIntBloomPort, COracle
+    from pebbledb_amd.keys import PackedKeys, splitmix_hex_keys
+    g = mine[0]
+    o = COracle()
+    t0 = time.perf_counter()
+    want = o.build(nb_bytes, k, PackedKeys.fixed(splitmix_hex_keys(SEED, g * n_f, n_f)), omp=True)
+    t_build = time.perf_counter() - t0
+    ns = 1_000_000
+    a = (len(q) // 16) // 2 - ns // 2
+    a -= a % 8
+    qs = PackedKeys.fixed(q[a * 16:(a + ns) * 16].cpu().numpy().reshape(-1, 16))
+    t0 = time.perf_counter()
+    hm = o.probe(want, k, qs, omp=True)
+    t_probe = time.perf_counter() - t0
+    gpu = hms[g].cpu().numpy()[a // 8:(a + ns) // 8]
+    # the reference's own algorithm on the full-size filter (each probe ANDs a 1<<idx big-int
+    # against the 2^30-bit int): a handful of probes in the budget
+    port = BigIntBloomPort(nb_bytes, k, bits=int.from_bytes(want.tobytes(), "little"))
+    t0 = time.perf_counter()
+    npb = 0
+    while time.perf_counter() - t0 < min(args.cpu_seconds, 8.0):
+        port.may_contain(qs.key(npb % ns).decode())
+        npb += 1
+    t_port = time.perf_counter() - t0
+    return {"value": round(npb / t_port / 1e6, 9), "unit": "Mprobes/s", "cores": 1, "kind": "port",
+            "sample": f"reference algorithm (BigIntBloomPort, Python big-int bitmap of 2^30 bits) probing filter {g}: "
+                      f"{npb} keys in {t_port:.1f}s",
+            "c_oracle_omp": {"value": round(ns / t_probe / 1e6, 2), "unit": "Mprobes/s", "cores": o.num_threads(),
+                             "sample": f"{ns} probes vs filter {g} (build of its {n_f} keys: {t_build:.2f}s)"},
+            "oracle_sample_equal": bool(np.array_equal(gpu, hm))}
+
+
 def sets_main(args, rank, world, local, torch, dist, np):
     """Configs 4 and 5: eight independent SSTable filters spread over the ranks (8/N each,
     shard.filters_for_rank), no collective on the data path.
@@ -296,10 +366,19 @@ def sets_main(args, rank, world, local, torch, dist, np):
         bf.sync()
         fp_rate = float(np.unpackbits(hm2.cpu().numpy()).sum()) / 1e6
     else:
+        fp_total, fp_expect = 0, 0.0
         for g in mine:
-            bits = np.unpackbits(hms[g].cpu().numpy(), bitorder="little")
+            bits = np.unpackbits(hms[g].cpu().numpy(), bitorder="little")[:nq]
             cnt = per if g < 7 else half - 7 * per
             ok &= bool(bits[g * per:g * per + cnt].all())
+            # the absent half: false positives at the filter's own rate (fill^k)
+            fill = filters[g].popcount() / (8 * nb_bytes)
+            fp_total += int(bits[half:].sum())
+            fp_expect += (nq - half) * fill ** k
+        fp_ok = fp_total <= 3 * fp_expect + 20 * len(mine)
+    host_c5 = None
+    if args.config == "c5" and not args.no_host_c5:
+        host_c5 = c5_host_resident(args, filters, mine, hms, q, nq, k, torch, np, L)
     if world > 1:
         elapsed = float(all_reduce_scalar(torch, dist, elapsed, dist.ReduceOp.MAX, torch.float64))
         ok = bool(all_reduce_scalar(torch, dist, 1 if ok else 0, dist.ReduceOp.MIN, torch.int32))
@@ -312,11 +391,15 @@ def sets_main(args, rank, world, local, torch, dist, np):
                     f"a step builds every filter once; filters {len(mine)}/rank")
             pk = "build pass of the rank's filters (clear + tiled build each, concurrent streams)"
         else:
-            b_pass = probe_bytes(nq, 16.0, k, False) * len(mine)
-            metric, unit = "Mprobes/s (key x filter) batched probe, 100M keys vs 8x128MiB filters", "Mprobes/s"
+            # the shared partition reads the keys ONCE for all of the rank's filters; each filter
+            # then costs its k 4-B bitmap reads per key and its hit mask (SURVEY.md §8d probe
+            # bytes, key term counted once): nq*L + nf*(4*nq*k + nq/8)
+            b_pass = nq * 16 + len(mine) * (4 * nq * k + nq // 8)
+            metric, unit = f"Mprobes/s (key x filter) batched probe, {nq // 1_000_000}M keys vs 8x128MiB filters", "Mprobes/s"
             what = (f"c5: {nq} probe keys (half members) x 8 filters (nb_bytes=2^27, k=6, 10M keys each); "
                     f"a step = one pbf_probe_multi over the rank's {len(mine)} filters")
-            pk = "multi-filter probe (shared k_part + per-filter k_tile_probe/k_gather)"
+            pk = ("multi-filter probe (shared k_part_ring + one XCD-aware k_tile_probe_set over every filter + "
+                  "one fused k_gather_ring<8>)")
         if args.config == "c4":
             # the rank's filters build concurrently on their own streams, so per-filter event
             # spans overlap: the pass rate is all of the rank's filters' bytes per step time
@@ -334,9 +417,19 @@ def sets_main(args, rank, world, local, torch, dist, np):
                          "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "kernel": pk,
                          "algorithmic_bytes": int(b_pass), "avg_ms": round(pass_ms, 4)},
             "check": {"members_all_hit": ok},
+            "rccl_world_size": dist.get_world_size() if world > 1 else 1,
+            "backend": (dist.get_backend() if world > 1 else None),
         }
         if fp_rate is not None:
             out["check"]["fp_rate_1M_absent"] = fp_rate
+        if args.config == "c5":
+            out["check"].update({"false_positives_rank0": fp_total, "fp_expected_rank0": round(fp_expect, 1),
+                                 "fp_within_3x_expected": bool(fp_ok), "probe_detail": hex(s0.last_probe_detail)})
+            if host_c5 is not None:
+                out["host_resident"] = host_c5
+            if world == 1 and not args.no_cpu_baseline:
+                out["cpu_baseline"] = c5_cpu_baseline(args, filters, mine, hms, q, n_f, nb_bytes, k, np)
+                out["check"]["oracle_sample_equal"] = out["cpu_baseline"].pop("oracle_sample_equal")
         if args.config == "c5":
             # the same work as independent single-filter probes (no shared partition)
             tq = []
@@ -437,18 +530,80 @@ def sst_main(args, rank, world, local, torch, dist, np):
     print(json.dumps(out_line), flush=True)
 
 
+def spawn_ranks(args) -> int:
+    """--gpus N without a launcher: start N ranks of this script (one per GPU) and wait.  Runs
+    before anything in this process touches a GPU (children are started, never exec'd into).
+    A rank that fails ends the others (they would wait at a barrier forever)."""
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0:
+                rc = rc or code
+                for other in live:
+                    other.terminate()
+        time.sleep(0.05)
+    return rc
+
+
+def dry_run(args, rank, world, dist):
+    """Launcher and plumbing check without a GPU: gloo rendezvous on 127.0.0.1, the barrier
+    and the max-over-ranks of the timed region as a real run does them.  Reports no number."""
+    import torch
+    if world > 1:
+        dist.init_process_group(backend="gloo", init_method="env://")
+        dist.barrier()
+    t0 = time.perf_counter()
+    time.sleep(0.01 * (rank + 1))
+    elapsed = time.perf_counter() - t0
+    seen = 1
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+        seen = dist.get_world_size()
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "metric": None, "value": None, "n_gpus": world, "world_size_seen": seen,
+                          "backend": "gloo" if world > 1 else None, "max_elapsed_s": round(elapsed, 4),
+                          "config": {"workload": args.config}}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"bench.py: WORLD_SIZE={world} but --gpus={args.gpus}: launch {args.gpus} ranks "
+              f"(or run without a launcher and let --gpus start them)", file=sys.stderr)
+        sys.exit(2)
+    if args.dry_run:
+        import torch.distributed as dist
+        dry_run(args, rank, world, dist)
+        return
     # rehearsal of the N-rank path on a one-GPU box: every rank on device PBF_BENCH_DEVICE,
     # rendezvous / max-over-ranks over gloo (PBF_BENCH_BACKEND=gloo); the driver's runs use
     # one GPU per rank over RCCL
     if os.environ.get("PBF_BENCH_DEVICE"):
         local = int(os.environ["PBF_BENCH_DEVICE"])
-    if world != args.gpus:
-        print(f"warning: WORLD_SIZE={world} but --gpus={args.gpus}", file=sys.stderr)
 
     import torch
     import torch.distributed as dist
@@ -556,6 +711,11 @@ def main():
     hm = hitmask.cpu().numpy()
     members_ok = bool((np.unpackbits(hm, bitorder="little")[:n] == 1).all())
     fp = int(np.unpackbits(hm, bitorder="little")[n:2 * n].sum())
+    # a corrupted bitmap (e.g. all ones) still lets every member hit: the absent half must show
+    # false positives at the filter's own rate, fill^k (fill measured on the device)
+    fill = bf.popcount() / m_bits
+    fp_expect = n * fill ** k
+    fp_ok = fp <= 3 * fp_expect + 20
     if world > 1:
         dist.barrier()
     elapsed = t1 - t0
@@ -569,6 +729,7 @@ def main():
     if world > 1:
         elapsed = float(all_reduce_scalar(torch, dist, elapsed, dist.ReduceOp.MAX, torch.float64))
         members_ok = bool(all_reduce_scalar(torch, dist, 1 if members_ok else 0, dist.ReduceOp.MIN, torch.int32))
+        fp_ok = bool(all_reduce_scalar(torch, dist, 1 if fp_ok else 0, dist.ReduceOp.MIN, torch.int32))
 
     host_inc = None
     if rank == 0 and offs is None and not args.no_host_inclusive:
@@ -593,7 +754,9 @@ def main():
         traffic = measured_traffic(args.config)
         dom_pass = "build" if build_ms >= probe_ms else "probe"
         out = {
-            "metric": "Mkeys/s bloom build+probe (device-resident), 10M 16B keys; 1/2/4/8 GPU",
+            "metric": ("Mkeys/s bloom build+probe (device-resident), 10M 16B keys; 1/2/4/8 GPU" if args.config == "c2"
+                       else f"Mkeys/s bloom build+probe (device-resident), {n} "
+                            f"{'16B' if kind == 'hex16' else 'variable-length (8-64 B)'} keys"),
             "value": round(value, 3),
             "unit": "Mkeys/s",
             "n_gpus": world,
@@ -604,7 +767,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u32",
-            "data": "synthetic (splitmix64 hex keys generated on device)",
+            "data": ("synthetic (splitmix64 hex keys generated on device)" if kind == "hex16" else
+                     "synthetic (splitmix64-derived [0-9a-z] keys of 8-64 B generated on device)"),
             "config": {"workload": f"{args.config}: build {n} keys of {key_bytes:.1f} B into m=2^{m_bits.bit_length() - 1}"
                                    f" bits (nb_bytes={nb_bytes}), k={k}; probe {2 * n} keys ({n} members + {n} absent)"
                                    f"; one filter per GPU", "n_build": n, "n_probe": 2 * n, "nb_bytes": nb_bytes, "k": k,
@@ -627,7 +791,10 @@ def main():
             "roofline_probe": {"achieved": round(ach_probe, 1), "frac": round(ach_probe / HBM_PEAK_GBS, 4),
                                "algorithmic_bytes": int(b_probe), "traffic": int(traffic["probe"]) if traffic else None},
             "traffic_source": traffic["source"] if traffic else "no PMC summary for this library build",
-            "check": {"members_all_hit": members_ok, "false_positives": fp, "probes_absent": n},
+            "check": {"members_all_hit": members_ok, "false_positives": fp, "probes_absent": n,
+                      "fp_expected": round(fp_expect, 2), "fp_within_3x_expected": bool(fp_ok)},
+            "rccl_world_size": dist.get_world_size() if world > 1 else 1,
+            "backend": (dist.get_backend() if world > 1 else None),
         }
         if host_inc is not None:
             out["host_inclusive"] = host_inc

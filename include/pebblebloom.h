@@ -18,10 +18,13 @@
  *     keys_on_device = 1: they are device pointers on the filter's device; the call is
  *     asynchronous on the filter's stream (pbf_stream) and the caller keeps them alive until
  *     pbf_sync (or an event recorded on that stream) completes.
- *   - A handle is one filter on one device with one HIP stream.  Calls on one handle are
- *     serialised by the caller; distinct handles may be driven from distinct host threads
- *     (the reference builds a filter under the flush mutex, lsm_storage.py:220, and only
- *     reads it afterwards, lsm_storage.py:164-179).
+ *   - A handle is one filter on one device with one HIP stream.  Every call takes the handle's
+ *     mutex, so one handle may be used from several host threads (the reference builds a
+ *     filter under the flush mutex, lsm_storage.py:220, and then probes it from any reader
+ *     thread without a lock, lsm_storage.py:153-179); distinct handles run concurrently.
+ *   - Working memory of the tiled pipelines and the host staging path is a per-device pool
+ *     shared by all handles (pbf_trim releases it), not per-filter: a long-lived filter holds
+ *     only its bitmap.
  */
 #ifndef PEBBLEBLOOM_H
 #define PEBBLEBLOOM_H
@@ -47,6 +50,11 @@ extern "C" {
 #define PBF_PROBE_AUTO 0
 #define PBF_PROBE_DIRECT 1 /* one lane per key, k random word loads, wave ballot */
 #define PBF_PROBE_TILED 2  /* partition (key, position) entries by LDS tile, test in LDS, gather */
+
+/* What the last probe ran (pbf_last_probe_detail): bit flags | (filters per fused gather << 8). */
+#define PBF_DETAIL_RING 1    /* tiled: ring partition (k_part_ring) */
+#define PBF_DETAIL_SORT 2    /* tiled: counting-sort partition (k_part) */
+#define PBF_DETAIL_ONE_KEY 4 /* pbf_may_contain's one-key launch */
 
 typedef struct pbf_filter pbf_filter_t;
 
@@ -93,6 +101,13 @@ int pbf_probe_multi_fixed(pbf_filter_t* const* filters, uint32_t nfilters, const
 int pbf_probe_multi(pbf_filter_t* const* filters, uint32_t nfilters, const uint8_t* keys, const uint64_t* offsets,
                     uint64_t n, uint8_t* const* hitmasks, int keys_on_device);
 
+/* BloomFilter.may_contain(key) for ONE key (bloom_filter.py:67-74), the per-key call of
+ * LsmStorage.get (lsm_storage.py:165,175): key is host memory (UTF-8 bytes, len may be 0),
+ * *out = 1 or 0.  Synchronous; the key goes to the kernel through mapped pinned memory and the
+ * hit byte comes back the same way (one launch, no copies, no allocation after the first call
+ * on a thread). */
+int pbf_may_contain(pbf_filter_t* f, const uint8_t* key, uint64_t len, int* out);
+
 /* The k bit indices of each key, BloomFilter._hash (bloom_filter.py:38-49): out[i*k + s] =
  * mmh3.hash(key_i, s) % bits_size (Python floor-mod).  out is host or device memory as
  * keys_on_device says (n*k uint64).  Used for index-math parity at any m. */
@@ -124,9 +139,15 @@ int pbf_set_build_mode(pbf_filter_t* f, int mode);
 int pbf_last_build_mode(pbf_filter_t* f);
 
 /* Select the probe strategy (PBF_PROBE_*); the one used by the last probe is returned by
- * pbf_last_probe_mode. */
+ * pbf_last_probe_mode, and how it ran by pbf_last_probe_detail (PBF_DETAIL_*). */
 int pbf_set_probe_mode(pbf_filter_t* f, int mode);
 int pbf_last_probe_mode(pbf_filter_t* f);
+uint32_t pbf_last_probe_detail(pbf_filter_t* f);
+
+/* Release the device's pooled working memory (waits for its last users); the next call
+ * re-allocates what it needs.  pbf_scratch_bytes reports what the pool holds now. */
+int pbf_trim(int device);
+int pbf_scratch_bytes(int device, uint64_t* out);
 
 /* SSTableBuilder's data section (src/sstable.py:224-268; DataBlock.to_bytes blocks.py:33-37;
  * Record.to_bytes record.py:66-72, key_size = the key's UTF-8 CHARACTER count as the reference's

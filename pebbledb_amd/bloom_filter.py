@@ -10,14 +10,21 @@ UTF-8 bytes, Python floor-mod of the signed hash by ``bits_size``.
 The bitmap lives in HBM behind a ``pbf_filter_t`` handle (libpebblebloom.so, ctypes).  Per-key
 ``add()`` calls are buffered on the host and sent as one batch at the next read (probe,
 serialisation, ``bits``), so an SSTableBuilder-style loop of ``add`` costs one kernel
-pipeline, not one launch per key.  Batch entry points ``add_many`` / ``may_contain_many`` take
-``list[str]`` or ``PackedKeys`` (host numpy) directly.
+pipeline, not one launch per key.  ``may_contain(key)`` — LsmStorage.get's per-key call — is
+one kernel launch that reads the key from mapped pinned memory (``pbf_may_contain``).  Batch
+entry points ``add_many`` / ``may_contain_many`` take ``list[str]``, ``PackedKeys`` or a
+``KeyPacker`` directly.
+
+Thread safety: the reference probes a filter from any reader thread without a lock
+(lsm_storage.py:153-179).  Here every native call takes the handle's mutex, and the host-side
+``add`` buffer has its own lock, so concurrent ``add`` / ``may_contain`` on one filter are safe.
 """
 from __future__ import annotations
 
 import ctypes
 import os
 import struct
+import threading
 from math import ceil, log
 from typing import Iterable, Optional
 
@@ -50,6 +57,7 @@ class BloomFilter:
         self.nb_hash_functions = nb_hash_functions
         self.device = _default_device if device is None else int(device)
         self._pending: list[str] = []
+        self._plock = threading.Lock()  # guards _pending (add / flush from several threads)
         self._h = None
         if nb_bytes > 0:
             h = ctypes.c_void_p()
@@ -77,15 +85,21 @@ class BloomFilter:
         return True
 
     def _upload_int(self, bits: int) -> None:
+        """The reference stores any int as ``bits`` and only ever reads its low 8*nb_bytes bits
+        (``to_bytes`` bloom_filter.py:78 and ``_is_bit_set`` with indices < bits_size): bits
+        outside that range (and a negative int's infinite sign extension) are dropped here."""
         if self.nb_bytes <= 0:
             raise ValueError("bits given for a filter with nb_bytes <= 0")
-        data = np.frombuffer(int(bits).to_bytes(self.nb_bytes, "little"), dtype=np.uint8)
+        masked = int(bits) & ((1 << (8 * self.nb_bytes)) - 1)
+        data = np.frombuffer(masked.to_bytes(self.nb_bytes, "little"), dtype=np.uint8)
         _native.check(_native.lib().pbf_set_bitmap(self._h, _vp(data), self.nb_bytes), "pbf_set_bitmap")
 
     def _flush(self) -> None:
         if self._pending:
-            pend, self._pending = self._pending, []
-            self._add_packed(PackedKeys.from_strs(pend))
+            with self._plock:
+                pend, self._pending = self._pending, []
+            if pend:
+                self._add_packed(PackedKeys.from_strs(pend))
 
     def _add_packed(self, pk: PackedKeys) -> None:
         if pk.n == 0 or not self._require_modulus():
@@ -132,7 +146,8 @@ class BloomFilter:
 
     @bits.setter
     def bits(self, value: int) -> None:
-        self._pending = []
+        with self._plock:
+            self._pending = []
         if self.nb_bytes > 0:
             _native.check(_native.lib().pbf_clear(self._h), "pbf_clear")
             if value:
@@ -167,13 +182,22 @@ class BloomFilter:
         """bloom_filter.py:60-65 (buffered; sent as one batch at the next read)."""
         if self.nb_hash_functions > 0:
             self._require_modulus()
-        self._pending.append(key)
-        if len(self._pending) >= _PENDING_FLUSH:
+        with self._plock:
+            self._pending.append(key)
+            full = len(self._pending) >= _PENDING_FLUSH
+        if full:
             self._flush()
 
     def may_contain(self, key: str) -> bool:
-        """bloom_filter.py:67-74."""
-        return bool(self._probe_packed(PackedKeys.from_strs([key]))[0] & 1)
+        """bloom_filter.py:67-74 — one key, one kernel launch (pbf_may_contain)."""
+        if not self._require_modulus():
+            return True  # k == 0: the AND over no bits
+        if self._pending:
+            self._flush()
+        out = ctypes.c_int(0)
+        enc = key.encode("utf-8")
+        _native.check(_native.lib().pbf_may_contain(self._h, enc, len(enc), ctypes.byref(out)), "pbf_may_contain")
+        return bool(out.value)
 
     def to_bytes(self) -> bytes:
         """bloom_filter.py:76-81: little-endian bitmap + one byte of k (struct.error if k > 255)."""
@@ -221,7 +245,8 @@ class BloomFilter:
     # are asynchronous on the filter's stream: keep the buffers alive and call sync() (or wait
     # on an event recorded on `stream`) before reading results or freeing inputs.
     def clear(self) -> None:
-        self._pending = []
+        with self._plock:
+            self._pending = []
         if self._h is not None:
             _native.check(_native.lib().pbf_clear(self._h), "pbf_clear")
 
@@ -278,6 +303,11 @@ class BloomFilter:
     @property
     def last_probe_mode(self) -> int:
         return 0 if self._h is None else _native.lib().pbf_last_probe_mode(self._h)
+
+    @property
+    def last_probe_detail(self) -> int:
+        """PBF_DETAIL_* flags of the last probe | (filters per fused gather << 8)."""
+        return 0 if self._h is None else int(_native.lib().pbf_last_probe_detail(self._h))
 
     @property
     def last_build_mode(self) -> int:

@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -52,7 +53,12 @@ struct DevBuf {
     size_t bytes = 0;
     hipError_t ensure(size_t want) {
         if (want <= bytes) return hipSuccess;
-        if (p) (void)hipFree(p);
+        if (p) {
+            // growth only: the old buffer may still be read by queued work on any stream
+            hipError_t s = hipDeviceSynchronize();
+            if (s != hipSuccess) return s;
+            (void)hipFree(p);
+        }
         p = nullptr;
         bytes = 0;
         hipError_t e = hipMalloc(&p, want);
@@ -106,6 +112,18 @@ int probe_rounds() {
         const char* e = std::getenv("PBF_PROBE_ROUNDS");
         const int x = e ? std::atoi(e) : 0;
         return x > 0 ? x : 1;
+    }();
+    return v;
+}
+
+// Keys per tiled-probe pipeline (PBF_PROBE_CHUNK overrides; 0 = as large as the plan allows).
+// Smaller pipelines keep one pipeline's region entries plus the bitmap inside the 256 MiB
+// Infinity Cache between the partition's writes and the tile test's / gather's reads.
+uint64_t probe_chunk() {
+    static const uint64_t v = [] {
+        const char* e = std::getenv("PBF_PROBE_CHUNK");
+        const long long x = e ? std::atoll(e) : 0;
+        return x > 0 ? (uint64_t(x) + 63) & ~uint64_t(63) : uint64_t(0);
     }();
     return v;
 }
@@ -203,6 +221,58 @@ uint32_t ceil_log2(uint64_t x) {
 
 }  // namespace
 
+namespace {
+
+// Transient working memory of the tiled pipelines and the host staging path.  It is not owned
+// by a filter: an LSM keeps one filter per SSTable alive for the SSTable's lifetime, and each
+// needs only its bitmap once built.  A device keeps a small pool of these sets; a call leases
+// one for the duration of its host-side enqueue, and the GPU-side reuse across streams is
+// ordered by the set's `last` event (the next user's stream waits on it).
+struct Scratch {
+    DevBuf regions, fill, ovf, ovf_count, subcnt, rbits, neg, alive, hw;
+    uint32_t ovf_phase = 0;  // which of the two overflow counters the next build uses
+    bool ovf_init = false;
+    DevBuf dkeys, doffs, dout;
+    PinBuf pin[2];
+    int pin_next = 0;
+    hipEvent_t last = nullptr;          // completion of the last user's work
+    hipStream_t last_stream = nullptr;  // ... on this stream
+    bool leased = false;
+    void release_all() {
+        for (DevBuf* d : {&regions, &fill, &ovf, &ovf_count, &subcnt, &rbits, &neg, &alive, &hw, &dkeys, &doffs, &dout})
+            d->release();
+        pin[0].release();
+        pin[1].release();
+        ovf_init = false;
+    }
+};
+
+struct DevicePool {
+    std::mutex mu;
+    std::vector<Scratch*> sets;
+};
+
+DevicePool& device_pool(int device) {
+    static std::mutex mu;
+    static std::map<int, DevicePool*> pools;
+    std::lock_guard<std::mutex> lock(mu);
+    auto& p = pools[device];
+    if (!p) p = new DevicePool();
+    return *p;
+}
+
+// Sets kept per device before a lease waits for an idle one (PBF_SCRATCH_SETS overrides).
+size_t max_scratch_sets() {
+    static const size_t v = [] {
+        const char* e = std::getenv("PBF_SCRATCH_SETS");
+        const int x = e ? std::atoi(e) : 0;
+        return x > 0 ? size_t(x) : size_t(8);
+    }();
+    return v;
+}
+
+}  // namespace
+
 struct pbf_filter {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -220,14 +290,12 @@ struct pbf_filter {
     bool tiled_ok = false;
     int probe_mode = PBF_PROBE_AUTO;
     int last_probe_mode = 0;
-    DevBuf regions, fill, ovf, ovf_count, subcnt, rbits, neg, alive, hw;
-    uint32_t ovf_phase = 0;  // which of the two overflow counters the next build uses
-    bool ovf_init = false;
-    DevBuf dkeys, doffs, dout;
-    PinBuf pin[2];
-    int pin_next = 0;
+    uint32_t last_probe_detail = 0;  // PBF_DETAIL_* of the last probe
+    Scratch* sc = nullptr;           // leased for the current call
     uint64_t* dpop = nullptr;
-    hipEvent_t ev = nullptr;  // stream joins of multi-filter probes
+    hipEvent_t ev = nullptr;       // stream joins of multi-filter probes
+    hipEvent_t done_ev = nullptr;  // blocking waits (pbf_sync)
+    std::mutex mu;                 // one host thread inside the handle at a time
 };
 
 namespace {
@@ -237,6 +305,62 @@ int enter(pbf_filter_t* f) {
     HIP_TRY(hipSetDevice(f->device));
     return PBF_OK;
 }
+
+// Lease a scratch set of f's device for work enqueued on f's stream (RAII).  Prefers a set
+// whose previous work is done or was on this same stream; creates one while fewer than
+// max_scratch_sets() exist; otherwise takes a free set and orders this stream after its
+// previous user.
+class Lease {
+   public:
+    Lease(pbf_filter_t* f) : f_(f) {}
+    int acquire() {
+        DevicePool& pool = device_pool(f_->device);
+        Scratch* pick = nullptr;
+        {
+            std::lock_guard<std::mutex> lock(pool.mu);
+            Scratch* any = nullptr;
+            for (Scratch* s : pool.sets) {
+                if (s->leased) continue;
+                if (!any) any = s;
+                if (!s->last || s->last_stream == f_->stream || hipEventQuery(s->last) == hipSuccess) {
+                    pick = s;
+                    break;
+                }
+            }
+            if (!pick && (pool.sets.size() < max_scratch_sets() || !any)) {
+                pick = new Scratch();
+                pool.sets.push_back(pick);
+            }
+            if (!pick) pick = any;
+            pick->leased = true;
+        }
+        s_ = pick;
+        if (!s_->last) HIP_TRY(hipEventCreateWithFlags(&s_->last, hipEventDisableTiming));
+        if (s_->last_stream && s_->last_stream != f_->stream) HIP_TRY(hipStreamWaitEvent(f_->stream, s_->last, 0));
+        f_->sc = s_;
+        return PBF_OK;
+    }
+    ~Lease() {
+        if (!s_) return;
+        // stream-order the set's next user after everything this call enqueued
+        if (hipEventRecord(s_->last, f_->stream) == hipSuccess) s_->last_stream = f_->stream;
+        f_->sc = nullptr;
+        DevicePool& pool = device_pool(f_->device);
+        std::lock_guard<std::mutex> lock(pool.mu);
+        s_->leased = false;
+    }
+
+   private:
+    pbf_filter_t* f_;
+    Scratch* s_ = nullptr;
+};
+
+#define LEASE(f)                        \
+    Lease lease_(f);                    \
+    do {                                \
+        int lrc_ = lease_.acquire();    \
+        if (lrc_) return lrc_;          \
+    } while (0)
 
 // Bring a pristine bitmap to its explicit all-zero form (before atomics / reads).
 int materialise(pbf_filter_t* f) {
@@ -417,20 +541,20 @@ int run_tiled(pbf_filter_t* f, const Batch& b) {
     const uint32_t k = f->k;
     const PartPlan pl = plan_for(tm, k, b.km, b.n, false);
     const PartGeom& pg = pl.pg;
-    HIP_TRY(f->regions.ensure(size_t(pg.G) * B * pg.cap * 4));
-    HIP_TRY(f->fill.ensure(size_t(pg.G) * B * 4));
-    HIP_TRY(f->ovf.ensure(std::max<uint64_t>(b.n * k, 1) * 4));
-    HIP_TRY(f->ovf_count.ensure(64));
-    if (!f->ovf_init) {  // two counters, used alternately; each build's k_ovf_build zeroes the other
-        HIP_TRY(hipMemsetAsync(f->ovf_count.p, 0, 64, f->stream));
-        f->ovf_init = true;
+    HIP_TRY(f->sc->regions.ensure(size_t(pg.G) * B * pg.cap * 4));
+    HIP_TRY(f->sc->fill.ensure(size_t(pg.G) * B * 4));
+    HIP_TRY(f->sc->ovf.ensure(std::max<uint64_t>(b.n * k, 1) * 4));
+    HIP_TRY(f->sc->ovf_count.ensure(64));
+    if (!f->sc->ovf_init) {  // two counters, used alternately; each build's k_ovf_build zeroes the other
+        HIP_TRY(hipMemsetAsync(f->sc->ovf_count.p, 0, 64, f->stream));
+        f->sc->ovf_init = true;
     }
-    auto* regions = static_cast<uint32_t*>(f->regions.p);
-    auto* fill = static_cast<uint32_t*>(f->fill.p);
-    auto* ovf = static_cast<uint32_t*>(f->ovf.p);
-    auto* ovf_count = static_cast<uint32_t*>(f->ovf_count.p) + f->ovf_phase;
-    uint32_t* ovf_next = static_cast<uint32_t*>(f->ovf_count.p) + (f->ovf_phase ^ 1);
-    f->ovf_phase ^= 1;
+    auto* regions = static_cast<uint32_t*>(f->sc->regions.p);
+    auto* fill = static_cast<uint32_t*>(f->sc->fill.p);
+    auto* ovf = static_cast<uint32_t*>(f->sc->ovf.p);
+    auto* ovf_count = static_cast<uint32_t*>(f->sc->ovf_count.p) + f->sc->ovf_phase;
+    uint32_t* ovf_next = static_cast<uint32_t*>(f->sc->ovf_count.p) + (f->sc->ovf_phase ^ 1);
+    f->sc->ovf_phase ^= 1;
     hipStream_t s = f->stream;
     hipError_t err = hipSuccess;
     dispatch(kmax_for(k), b.km, [&](auto KMAX, auto KM) {
@@ -477,28 +601,29 @@ int run_tiled_probe_set(pbf_filter_t* f, pbf_filter_t* const* fs, uint32_t nf, c
     const PartPlan pl = plan_for(tm, k, b.km, b.n, true, nf);
     const PartGeom& pg = pl.pg;
     const uint32_t nfg = pg.ring ? nf : 1;  // filters per gather launch (R and hw copies)
-    HIP_TRY(f->regions.ensure(size_t(pg.G) * B * pg.cap * 4));
-    HIP_TRY(f->fill.ensure(size_t(pg.G) * B * 4));
+    f->last_probe_detail = (pg.ring ? PBF_DETAIL_RING : PBF_DETAIL_SORT) | (nfg << 8);
+    HIP_TRY(f->sc->regions.ensure(size_t(pg.G) * B * pg.cap * 4));
+    HIP_TRY(f->sc->fill.ensure(size_t(pg.G) * B * 4));
     // sort partition: per-sub-chunk tile counts; ring partition: cumulative counts per 4 sub-chunks
-    HIP_TRY(f->subcnt.ensure(pg.ring ? size_t(pg.G) * B * (pg.nq + 1) * 4 : size_t(pg.G) * pg.nsub * B * 4));
+    HIP_TRY(f->sc->subcnt.ensure(pg.ring ? size_t(pg.G) * B * (pg.nq + 1) * 4 : size_t(pg.G) * pg.nsub * B * 4));
     const size_t r_words = size_t(pg.G) * B * (pg.cap / 32);
-    HIP_TRY(f->rbits.ensure(r_words * 4 * nfg));
+    HIP_TRY(f->sc->rbits.ensure(r_words * 4 * nfg));
     const uint64_t neg_words = (b.n + 31) / 32;
     const size_t neg_bytes = neg_words * 4;
-    HIP_TRY(f->neg.ensure(neg_bytes * nf));
-    auto* regions = static_cast<uint32_t*>(f->regions.p);
-    auto* fill = static_cast<uint32_t*>(f->fill.p);
-    auto* subcnt = static_cast<uint32_t*>(f->subcnt.p);
-    auto* R = static_cast<uint32_t*>(f->rbits.p);
-    auto* neg = static_cast<uint32_t*>(f->neg.p);
+    HIP_TRY(f->sc->neg.ensure(neg_bytes * nf));
+    auto* regions = static_cast<uint32_t*>(f->sc->regions.p);
+    auto* fill = static_cast<uint32_t*>(f->sc->fill.p);
+    auto* subcnt = static_cast<uint32_t*>(f->sc->subcnt.p);
+    auto* R = static_cast<uint32_t*>(f->sc->rbits.p);
+    auto* neg = static_cast<uint32_t*>(f->sc->neg.p);
     hipStream_t s = f->stream;
     // gather split over S tile ranges (several small workgroups per CU)
     const uint32_t S = pl.gsplit;
     const bool use_hw = S > 1 || nfg > 1;
     uint32_t* hw = nullptr;
     if (use_hw) {
-        HIP_TRY(f->hw.ensure(neg_bytes * nfg));
-        hw = static_cast<uint32_t*>(f->hw.p);
+        HIP_TRY(f->sc->hw.ensure(neg_bytes * nfg));
+        hw = static_cast<uint32_t*>(f->sc->hw.p);
     }
     ProbeSet ps{};
     ps.nf = nf;
@@ -544,11 +669,16 @@ int run_tiled_probe_set(pbf_filter_t* f, pbf_filter_t* const* fs, uint32_t nf, c
         else HIP_TRY(allow_lds(k_gather, pl.lds_gather));
         const dim3 grid(pg.G, S);
         if (pg.ring) {
-            // every filter's tile test, then ONE gather over the shared region entries
-            for (uint32_t i = 0; i < nf; ++i) {
-                k_tile_probe<<<B, 1024, lds_tile, s>>>(tm, pg, regions, fill, fs[i]->bitmap, R + i * r_words, expand);
-                CHECK_LAUNCH();
+            // every filter's tile test (one XCD-aware launch for a set), then ONE gather over
+            // the shared region entries
+            if (nf == 1) {
+                k_tile_probe<<<B, 1024, lds_tile, s>>>(tm, pg, regions, fill, fs[0]->bitmap, R, expand);
+            } else {
+                HIP_TRY(allow_lds(k_tile_probe_set, lds_tile));
+                const uint32_t grid = ((B + 7) / 8) * 8 * nf;
+                k_tile_probe_set<<<grid, 1024, lds_tile, s>>>(tm, pg, regions, fill, ps, R, r_words, expand);
             }
+            CHECK_LAUNCH();
             gring<<<grid, 512, pl.lds_gather, s>>>(tm, pg, b.n, regions, R, fill, subcnt, neg, alive, outs[0] + hm_off,
                                                   hw, nf, r_words, neg_words);
             CHECK_LAUNCH();
@@ -577,8 +707,8 @@ int run_tiled_probe_set(pbf_filter_t* f, pbf_filter_t* const* fs, uint32_t nf, c
     };
     if (nf > 1 || !pg.ring || k < 2 || probe_rounds() < 2) return round(0, k, nullptr, hitmasks);
     // two rounds: seed 0 for every key, then seeds 1..k-1 for the keys seed 0 left alive
-    HIP_TRY(f->alive.ensure(neg_bytes));
-    auto* alive = static_cast<uint32_t*>(f->alive.p);
+    HIP_TRY(f->sc->alive.ensure(neg_bytes));
+    auto* alive = static_cast<uint32_t*>(f->sc->alive.p);
     uint8_t* alive_out[1] = {reinterpret_cast<uint8_t*>(alive)};
     const uint64_t keep_off = hm_off;
     hm_off = 0;
@@ -626,6 +756,7 @@ bool want_tiled_probe(pbf_filter_t* f, uint64_t n) {
 uint64_t tiled_probe_batch(pbf_filter_t* f, int km, uint32_t nf = 1) {
     const uint32_t k = f->k;
     uint64_t n = std::max<uint64_t>(64, (kMaxPositions / k) & ~uint64_t(63));
+    if (probe_chunk()) n = std::min(n, probe_chunk());
     for (;;) {
         const PartPlan pl = plan_for(f->tm, k, km, n, true, nf);
         if ((pl.lds_gather <= 156 * 1024 && pl.pg.cap <= 65535) || n <= 64 * 1024) return n;
@@ -681,6 +812,7 @@ int probe_device(pbf_filter_t* f, const Batch& b, uint8_t* hitmask_dev) {
     });
     CHECK_LAUNCH();
     f->last_probe_mode = PBF_PROBE_DIRECT;
+    f->last_probe_detail = 0;
     return PBF_OK;
 }
 
@@ -737,11 +869,21 @@ int probe_multi_device(pbf_filter_t* const* fs, uint32_t nf, const Batch& b, uin
                 if (rc) return rc;
             }
         }
-        for (uint32_t i = 0; i < nf; ++i) fs[i]->last_probe_mode = PBF_PROBE_TILED;
-    } else {
-        // each filter on its own stream (and scratch), joined back into fs[0]'s
         for (uint32_t i = 0; i < nf; ++i) {
-            rc = probe_device(fs[i], b, hitmasks[i]);
+            fs[i]->last_probe_mode = PBF_PROBE_TILED;
+            fs[i]->last_probe_detail = f0->last_probe_detail;
+        }
+    } else {
+        // each filter on its own stream and scratch set (fs[0] uses the caller's lease),
+        // joined back into fs[0]'s
+        for (uint32_t i = 0; i < nf; ++i) {
+            if (i == 0) {
+                rc = probe_device(fs[0], b, hitmasks[0]);
+            } else {
+                Lease li(fs[i]);
+                rc = li.acquire();
+                if (!rc) rc = probe_device(fs[i], b, hitmasks[i]);
+            }
             if (rc) return rc;
         }
         for (uint32_t i = 1; i < nf; ++i) {
@@ -797,7 +939,14 @@ int for_host_chunks(pbf_filter_t* f, const uint8_t* keys, const uint64_t* offset
                     if (offsets[mid] - start <= stage_bytes()) lo = mid; else hi = mid - 1;
                 }
                 i1 = lo;
-                if (i1 - i0 > key_align) i1 = i0 + ((i1 - i0) / key_align) * key_align;
+                // every chunk but the last holds a multiple of key_align keys, so the next one
+                // starts on a whole hit-mask byte (probes: 64); when fewer than key_align keys
+                // fit the byte budget the chunk takes key_align keys anyway (staging buffers are
+                // sized from the chunk's actual bytes)
+                if (i1 - i0 >= key_align)
+                    i1 = i0 + ((i1 - i0) / key_align) * key_align;
+                else
+                    i1 = std::min<uint64_t>(n, i0 + key_align);
             }
         } else {
             uint64_t per = std::max<uint64_t>(1, stage_bytes() / std::max<uint32_t>(1, key_len));
@@ -809,31 +958,31 @@ int for_host_chunks(pbf_filter_t* f, const uint8_t* keys, const uint64_t* offset
         const uint64_t nbytes = offsets ? offsets[i1] - offsets[i0] : cn * key_len;
         const size_t off_bytes = offsets ? size_t(cn + 1) * 8 : 0;
         // device staging (single buffer: stream order serialises reuse)
-        HIP_TRY(f->dkeys.ensure(((nbytes + 15) & ~uint64_t(15)) + 16));
-        if (offsets) HIP_TRY(f->doffs.ensure(off_bytes));
+        HIP_TRY(f->sc->dkeys.ensure(((nbytes + 15) & ~uint64_t(15)) + 16));
+        if (offsets) HIP_TRY(f->sc->doffs.ensure(off_bytes));
         if (pinned) {
             // caller's buffers are page-locked: DMA straight from them (the call syncs before
             // returning, so they stay valid for the copy)
-            if (nbytes) HIP_TRY(hipMemcpyAsync(f->dkeys.p, keys + byte0, nbytes, hipMemcpyHostToDevice, f->stream));
+            if (nbytes) HIP_TRY(hipMemcpyAsync(f->sc->dkeys.p, keys + byte0, nbytes, hipMemcpyHostToDevice, f->stream));
             if (offsets)
-                HIP_TRY(hipMemcpyAsync(f->doffs.p, offsets + i0, off_bytes, hipMemcpyHostToDevice, f->stream));
+                HIP_TRY(hipMemcpyAsync(f->sc->doffs.p, offsets + i0, off_bytes, hipMemcpyHostToDevice, f->stream));
         } else {
-            PinBuf& pb = f->pin[f->pin_next];
-            f->pin_next ^= 1;
+            PinBuf& pb = f->sc->pin[f->sc->pin_next];
+            f->sc->pin_next ^= 1;
             if (pb.done) HIP_TRY(hipEventSynchronize(pb.done));
             HIP_TRY(pb.ensure(nbytes + off_bytes + 16));
             if (!pb.done) HIP_TRY(hipEventCreateWithFlags(&pb.done, hipEventDisableTiming));
             const size_t off_at = (nbytes + 15) & ~uint64_t(15);
             std::memcpy(pb.p, keys + byte0, nbytes);
             if (offsets) std::memcpy(static_cast<uint8_t*>(pb.p) + off_at, offsets + i0, off_bytes);
-            HIP_TRY(hipMemcpyAsync(f->dkeys.p, pb.p, nbytes, hipMemcpyHostToDevice, f->stream));
+            HIP_TRY(hipMemcpyAsync(f->sc->dkeys.p, pb.p, nbytes, hipMemcpyHostToDevice, f->stream));
             if (offsets)
-                HIP_TRY(hipMemcpyAsync(f->doffs.p, static_cast<uint8_t*>(pb.p) + off_at, off_bytes,
+                HIP_TRY(hipMemcpyAsync(f->sc->doffs.p, static_cast<uint8_t*>(pb.p) + off_at, off_bytes,
                                        hipMemcpyHostToDevice, f->stream));
             HIP_TRY(hipEventRecord(pb.done, f->stream));
         }
-        Batch b = make_batch(static_cast<const uint8_t*>(f->dkeys.p),
-                             offsets ? static_cast<const uint64_t*>(f->doffs.p) : nullptr, key_len, cn);
+        Batch b = make_batch(static_cast<const uint8_t*>(f->sc->dkeys.p),
+                             offsets ? static_cast<const uint64_t*>(f->sc->doffs.p) : nullptr, key_len, cn);
         int rc = op(b, i0);
         if (rc) return rc;
         i0 = i1;
@@ -854,37 +1003,72 @@ int check_keys(pbf_filter_t* f, const uint8_t* keys, const uint64_t* offsets, ui
     return PBF_OK;
 }
 
+// Wait for everything queued on f's stream.  Polls first (a caller that waits is about to use
+// the results, and a blocking wake-up costs tens of microseconds), then blocks on an event
+// created with hipEventBlockingSync, so a long wait does not keep a host core spinning
+// (PBF_SPIN_US sets the polling budget, default 200 us).
+int wait_stream(pbf_filter_t* f) {
+    static const long spin_us = [] {
+        const char* e = std::getenv("PBF_SPIN_US");
+        return e ? std::atol(e) : 200L;
+    }();
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+        const hipError_t e = hipStreamQuery(f->stream);
+        if (e == hipSuccess) return PBF_OK;
+        if (e != hipErrorNotReady) return fail(PBF_ERR_HIP, std::string("hipStreamQuery: ") + hipGetErrorString(e));
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(spin_us)) break;
+    }
+    if (!f->done_ev) HIP_TRY(hipEventCreateWithFlags(&f->done_ev, hipEventBlockingSync | hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(f->done_ev, f->stream));
+    HIP_TRY(hipEventSynchronize(f->done_ev));
+    return PBF_OK;
+}
+
+#define WAIT(f)                       \
+    do {                              \
+        int wrc_ = wait_stream(f);    \
+        if (wrc_) return wrc_;        \
+    } while (0)
+
+// Every entry point that touches a handle holds its mutex: the reference probes one filter from
+// many reader threads without a lock (lsm_storage.py:153-179), and a call's host-side state
+// (the leased scratch, staging, pending modes) must not be shared between two of them.
+#define LOCK(f)                                                         \
+    if (!(f)) return fail(PBF_ERR_INVALID, "null filter handle");       \
+    std::lock_guard<std::mutex> lock_((f)->mu)
+
 int add_impl(pbf_filter_t* f, const uint8_t* keys, const uint64_t* offsets, uint32_t key_len, uint64_t n,
              int on_device) {
+    LOCK(f);
     int rc = check_keys(f, keys, offsets, key_len, n, offsets != nullptr);
     if (rc || n == 0) return rc;
-    if (on_device) {
-        return add_device(f, make_batch(keys, offsets, key_len, n));
-    }
+    LEASE(f);
+    if (on_device) return add_device(f, make_batch(keys, offsets, key_len, n));
     rc = for_host_chunks(f, keys, offsets, key_len, n, 1, [&](const Batch& b, uint64_t) { return add_device(f, b); });
     if (rc) return rc;
-    HIP_TRY(hipStreamSynchronize(f->stream));
+    WAIT(f);
     return PBF_OK;
 }
 
 int probe_impl(pbf_filter_t* f, const uint8_t* keys, const uint64_t* offsets, uint32_t key_len, uint64_t n,
                uint8_t* hitmask, int on_device) {
+    LOCK(f);
     int rc = check_keys(f, keys, offsets, key_len, n, offsets != nullptr);
     if (rc || n == 0) return rc;
     if (!hitmask) return fail(PBF_ERR_INVALID, "null hitmask");
-    if (on_device) {
-        return probe_device(f, make_batch(keys, offsets, key_len, n), hitmask);
-    }
+    LEASE(f);
+    if (on_device) return probe_device(f, make_batch(keys, offsets, key_len, n), hitmask);
     rc = for_host_chunks(f, keys, offsets, key_len, n, 64, [&](const Batch& b, uint64_t i0) {
-        HIP_TRY(f->dout.ensure((b.n + 7) / 8 + 8));
-        int r = probe_device(f, b, static_cast<uint8_t*>(f->dout.p));
+        HIP_TRY(f->sc->dout.ensure((b.n + 7) / 8 + 8));
+        int r = probe_device(f, b, static_cast<uint8_t*>(f->sc->dout.p));
         if (r) return r;
-        HIP_TRY(hipMemcpyAsync(hitmask + i0 / 8, f->dout.p, (b.n + 7) / 8, hipMemcpyDeviceToHost, f->stream));
-        HIP_TRY(hipStreamSynchronize(f->stream));
+        HIP_TRY(hipMemcpyAsync(hitmask + i0 / 8, f->sc->dout.p, (b.n + 7) / 8, hipMemcpyDeviceToHost, f->stream));
+        WAIT(f);
         return PBF_OK;
     });
     if (rc) return rc;
-    HIP_TRY(hipStreamSynchronize(f->stream));
+    WAIT(f);
     return PBF_OK;
 }
 
@@ -899,43 +1083,52 @@ int probe_multi_impl(pbf_filter_t* const* fs, uint32_t nf, const uint8_t* keys, 
         for (uint32_t j = 0; j < i; ++j)
             if (fs[j] == fs[i]) return fail(PBF_ERR_INVALID, "a filter appears twice in the set");
     }
+    // every handle of the set, in address order (two overlapping sets cannot deadlock)
+    std::vector<pbf_filter_t*> order(fs, fs + nf);
+    std::sort(order.begin(), order.end());
+    std::vector<std::unique_lock<std::mutex>> locks;
+    locks.reserve(nf);
+    for (pbf_filter_t* p : order) locks.emplace_back(p->mu);
     int rc = check_keys(fs[0], keys, offsets, key_len, n, offsets != nullptr);
     if (rc || n == 0) return rc;
-    if (on_device) return probe_multi_device(fs, nf, make_batch(keys, offsets, key_len, n), hitmasks);
     pbf_filter_t* f0 = fs[0];
+    LEASE(f0);
+    if (on_device) return probe_multi_device(fs, nf, make_batch(keys, offsets, key_len, n), hitmasks);
     std::vector<uint8_t*> douts(nf);
     rc = for_host_chunks(f0, keys, offsets, key_len, n, 64, [&](const Batch& b, uint64_t i0) {
         const size_t stride = (((b.n + 7) / 8) + 255) & ~size_t(255);
-        HIP_TRY(f0->dout.ensure(stride * nf + 8));
-        for (uint32_t i = 0; i < nf; ++i) douts[i] = static_cast<uint8_t*>(f0->dout.p) + i * stride;
+        HIP_TRY(f0->sc->dout.ensure(stride * nf + 8));
+        for (uint32_t i = 0; i < nf; ++i) douts[i] = static_cast<uint8_t*>(f0->sc->dout.p) + i * stride;
         int r = probe_multi_device(fs, nf, b, douts.data());
         if (r) return r;
         for (uint32_t i = 0; i < nf; ++i)
             HIP_TRY(hipMemcpyAsync(hitmasks[i] + i0 / 8, douts[i], (b.n + 7) / 8, hipMemcpyDeviceToHost, f0->stream));
-        HIP_TRY(hipStreamSynchronize(f0->stream));
+        WAIT(f0);
         return PBF_OK;
     });
     if (rc) return rc;
-    HIP_TRY(hipStreamSynchronize(f0->stream));
+    WAIT(f0);
     return PBF_OK;
 }
 
 int hash_impl(pbf_filter_t* f, const uint8_t* keys, const uint64_t* offsets, uint32_t key_len, uint64_t n,
               uint64_t* out, int on_device) {
+    LOCK(f);
     int rc = check_keys(f, keys, offsets, key_len, n, offsets != nullptr);
     if (rc || n == 0) return rc;
     if (!out) return fail(PBF_ERR_INVALID, "null output");
     if (on_device) return hash_device(f, make_batch(keys, offsets, key_len, n), out);
+    LEASE(f);
     rc = for_host_chunks(f, keys, offsets, key_len, n, 1, [&](const Batch& b, uint64_t i0) {
-        HIP_TRY(f->dout.ensure(b.n * f->k * 8 + 8));
-        int r = hash_device(f, b, static_cast<uint64_t*>(f->dout.p));
+        HIP_TRY(f->sc->dout.ensure(b.n * f->k * 8 + 8));
+        int r = hash_device(f, b, static_cast<uint64_t*>(f->sc->dout.p));
         if (r) return r;
-        HIP_TRY(hipMemcpyAsync(out + i0 * f->k, f->dout.p, b.n * f->k * 8, hipMemcpyDeviceToHost, f->stream));
-        HIP_TRY(hipStreamSynchronize(f->stream));
+        HIP_TRY(hipMemcpyAsync(out + i0 * f->k, f->sc->dout.p, b.n * f->k * 8, hipMemcpyDeviceToHost, f->stream));
+        WAIT(f);
         return PBF_OK;
     });
     if (rc) return rc;
-    HIP_TRY(hipStreamSynchronize(f->stream));
+    WAIT(f);
     return PBF_OK;
 }
 
@@ -964,6 +1157,34 @@ EncodeCtx& encode_ctx(int device) {
     auto& p = ctx[device];
     if (!p) p = new EncodeCtx();
     return *p;
+}
+
+// Mapped, coherent pinned memory for the one-key probe (pbf_may_contain): result byte at 0,
+// offsets at kOneKeyOffs, key bytes at kOneKeyData (16-B aligned).  One per (thread, device):
+// calls from different threads never share it; it lives as long as the thread.
+constexpr size_t kOneKeyOffs = 64, kOneKeyData = 128, kOneKeyMax = 4096;
+struct OneKeyStage {
+    uint8_t* host = nullptr;
+    uint8_t* dev = nullptr;
+};
+
+int one_key_stage(int device, OneKeyStage** out) {
+    thread_local std::map<int, OneKeyStage> stages;
+    OneKeyStage& st = stages[device];
+    if (!st.host) {
+        void* h = nullptr;
+        HIP_TRY(hipHostMalloc(&h, kOneKeyData + kOneKeyMax + 64, hipHostMallocMapped | hipHostMallocCoherent));
+        void* d = nullptr;
+        const hipError_t e = hipHostGetDevicePointer(&d, h, 0);
+        if (e != hipSuccess) {
+            (void)hipHostFree(h);
+            return fail(PBF_ERR_HIP, std::string("hipHostGetDevicePointer: ") + hipGetErrorString(e));
+        }
+        st.host = static_cast<uint8_t*>(h);
+        st.dev = static_cast<uint8_t*>(d);
+    }
+    *out = &st;
+    return PBF_OK;
 }
 
 }  // namespace
@@ -1040,22 +1261,50 @@ int pbf_destroy(pbf_filter_t* f) {
     if (!f) return PBF_OK;
     (void)hipSetDevice(f->device);
     if (f->stream) (void)hipStreamSynchronize(f->stream);
+    {
+        // scratch sets last used on this stream: their work is done (synchronised above), and
+        // the stream handle may be reused by a later filter
+        DevicePool& pool = device_pool(f->device);
+        std::lock_guard<std::mutex> lock(pool.mu);
+        for (Scratch* sc : pool.sets)
+            if (sc->last_stream == f->stream) sc->last_stream = nullptr;
+    }
     if (f->bitmap) (void)hipFree(f->bitmap);
     if (f->dpop) (void)hipFree(f->dpop);
-    for (DevBuf* d : {&f->regions, &f->fill, &f->ovf, &f->ovf_count, &f->subcnt, &f->rbits, &f->neg, &f->alive, &f->hw})
-        d->release();
-    f->dkeys.release();
-    f->doffs.release();
-    f->dout.release();
-    f->pin[0].release();
-    f->pin[1].release();
     if (f->ev) (void)hipEventDestroy(f->ev);
+    if (f->done_ev) (void)hipEventDestroy(f->done_ev);
     if (f->stream) (void)hipStreamDestroy(f->stream);
     delete f;
     return PBF_OK;
 }
 
+int pbf_trim(int device) {
+    HIP_TRY(hipSetDevice(device));
+    DevicePool& pool = device_pool(device);
+    std::lock_guard<std::mutex> lock(pool.mu);
+    for (Scratch* sc : pool.sets) {
+        if (sc->leased) continue;
+        if (sc->last) HIP_TRY(hipEventSynchronize(sc->last));
+        sc->release_all();
+    }
+    return PBF_OK;
+}
+
+int pbf_scratch_bytes(int device, uint64_t* out) {
+    if (!out) return fail(PBF_ERR_INVALID, "null out");
+    DevicePool& pool = device_pool(device);
+    std::lock_guard<std::mutex> lock(pool.mu);
+    uint64_t t = 0;
+    for (Scratch* sc : pool.sets)
+        for (const DevBuf* d : {&sc->regions, &sc->fill, &sc->ovf, &sc->ovf_count, &sc->subcnt, &sc->rbits, &sc->neg,
+                                &sc->alive, &sc->hw, &sc->dkeys, &sc->doffs, &sc->dout})
+            t += d->bytes;
+    *out = t;
+    return PBF_OK;
+}
+
 int pbf_clear(pbf_filter_t* f) {
+    LOCK(f);
     int rc = enter(f);
     if (rc) return rc;
     if (f->tiled_ok) {
@@ -1079,16 +1328,18 @@ int pbf_clear(pbf_filter_t* f) {
 int pbf_add_fixed(pbf_filter_t* f, const uint8_t* keys, uint32_t key_len, uint64_t n, int on_device) {
     if (key_len == 0 && n > 0) {
         // n empty keys: the variable-length path with all-equal offsets
+        LOCK(f);
         int rc = enter(f);
         if (rc) return rc;
         if (f->k == 0) return PBF_OK;
-        HIP_TRY(f->doffs.ensure((n + 1) * 8));
-        HIP_TRY(hipMemsetAsync(f->doffs.p, 0, (n + 1) * 8, f->stream));
-        HIP_TRY(f->dkeys.ensure(16));
-        rc = add_device(f, make_batch(static_cast<const uint8_t*>(f->dkeys.p),
-                                      static_cast<const uint64_t*>(f->doffs.p), 0, n));
+        LEASE(f);
+        HIP_TRY(f->sc->doffs.ensure((n + 1) * 8));
+        HIP_TRY(hipMemsetAsync(f->sc->doffs.p, 0, (n + 1) * 8, f->stream));
+        HIP_TRY(f->sc->dkeys.ensure(16));
+        rc = add_device(f, make_batch(static_cast<const uint8_t*>(f->sc->dkeys.p),
+                                      static_cast<const uint64_t*>(f->sc->doffs.p), 0, n));
         if (rc) return rc;
-        if (!on_device) HIP_TRY(hipStreamSynchronize(f->stream));
+        if (!on_device) WAIT(f);
         return PBF_OK;
     }
     return add_impl(f, keys, nullptr, key_len, n, on_device);
@@ -1137,6 +1388,7 @@ int pbf_hash_indices(pbf_filter_t* f, const uint8_t* keys, const uint64_t* offse
 }
 
 int pbf_get_bitmap(pbf_filter_t* f, uint8_t* out, uint64_t nb_bytes) {
+    LOCK(f);
     int rc = enter(f);
     if (rc) return rc;
     if (nb_bytes != f->nb_bytes) return fail(PBF_ERR_INVALID, "nb_bytes mismatch");
@@ -1144,11 +1396,12 @@ int pbf_get_bitmap(pbf_filter_t* f, uint8_t* out, uint64_t nb_bytes) {
     rc = materialise(f);
     if (rc) return rc;
     HIP_TRY(hipMemcpyAsync(out, f->bitmap, nb_bytes, hipMemcpyDeviceToHost, f->stream));
-    HIP_TRY(hipStreamSynchronize(f->stream));
+    WAIT(f);
     return PBF_OK;
 }
 
 int pbf_set_bitmap(pbf_filter_t* f, const uint8_t* in, uint64_t nb_bytes) {
+    LOCK(f);
     int rc = enter(f);
     if (rc) return rc;
     if (nb_bytes != f->nb_bytes) return fail(PBF_ERR_INVALID, "nb_bytes mismatch");
@@ -1157,13 +1410,14 @@ int pbf_set_bitmap(pbf_filter_t* f, const uint8_t* in, uint64_t nb_bytes) {
         HIP_TRY(hipMemsetAsync(reinterpret_cast<uint8_t*>(f->bitmap) + nb_bytes, 0, f->alloc_words * 4 - nb_bytes,
                                f->stream));
     HIP_TRY(hipMemcpyAsync(f->bitmap, in, nb_bytes, hipMemcpyHostToDevice, f->stream));
-    HIP_TRY(hipStreamSynchronize(f->stream));
+    WAIT(f);
     f->pristine = false;
     f->middle_dirty = f->tm.cspace != 0;
     return PBF_OK;
 }
 
 int pbf_popcount(pbf_filter_t* f, uint64_t* out) {
+    LOCK(f);
     int rc = enter(f);
     if (rc) return rc;
     if (!out) return fail(PBF_ERR_INVALID, "null out");
@@ -1174,20 +1428,69 @@ int pbf_popcount(pbf_filter_t* f, uint64_t* out) {
         f->bitmap, f->alloc_words, reinterpret_cast<unsigned long long*>(f->dpop));
     CHECK_LAUNCH();
     HIP_TRY(hipMemcpyAsync(out, f->dpop, 8, hipMemcpyDeviceToHost, f->stream));
-    HIP_TRY(hipStreamSynchronize(f->stream));
+    WAIT(f);
     return PBF_OK;
 }
 
 int pbf_sync(pbf_filter_t* f) {
+    LOCK(f);
     int rc = enter(f);
     if (rc) return rc;
-    // Spin on the stream instead of a blocking wait: the caller is about to use the results,
-    // and a blocking synchronise can add milliseconds of wake-up latency.
-    for (;;) {
-        const hipError_t e = hipStreamQuery(f->stream);
-        if (e == hipSuccess) break;
-        if (e != hipErrorNotReady) return fail(PBF_ERR_HIP, std::string("hipStreamQuery: ") + hipGetErrorString(e));
+    return wait_stream(f);
+}
+
+int pbf_may_contain(pbf_filter_t* f, const uint8_t* key, uint64_t len, int* out) {
+    LOCK(f);
+    int rc = enter(f);
+    if (rc) return rc;
+    if (!out || (len && !key)) return fail(PBF_ERR_INVALID, "null key or out");
+    if (f->k == 0) {  // the AND over no bits (bloom_filter.py:71-74 runs no iteration)
+        *out = 1;
+        return PBF_OK;
     }
+    rc = materialise(f);
+    if (rc) return rc;
+    if (len > kOneKeyMax) {  // long keys: the staged batch path
+        uint64_t offs[2] = {0, len};
+        uint8_t hm = 0;
+        LEASE(f);
+        rc = for_host_chunks(f, key, offs, 0, 1, 64, [&](const Batch& b, uint64_t) {
+            HIP_TRY(f->sc->dout.ensure(8));
+            int r = probe_device(f, b, static_cast<uint8_t*>(f->sc->dout.p));
+            if (r) return r;
+            HIP_TRY(hipMemcpyAsync(&hm, f->sc->dout.p, 1, hipMemcpyDeviceToHost, f->stream));
+            return PBF_OK;
+        });
+        if (rc) return rc;
+        WAIT(f);
+        *out = hm & 1;
+        return PBF_OK;
+    }
+    OneKeyStage* st = nullptr;
+    rc = one_key_stage(f->device, &st);
+    if (rc) return rc;
+    // the key and its two offsets go into mapped pinned memory the kernel reads over the bus;
+    // the kernel's hit byte comes back the same way: one launch, no copies
+    uint64_t* offs = reinterpret_cast<uint64_t*>(st->host + kOneKeyOffs);
+    offs[0] = 0;
+    offs[1] = len;
+    if (len) std::memcpy(st->host + kOneKeyData, key, len);
+    st->host[0] = 0xEE;
+    KeySet ks{};
+    ks.data = st->dev + kOneKeyData;
+    ks.offsets = reinterpret_cast<const uint64_t*>(st->dev + kOneKeyOffs);
+    ks.off0 = ks.offsets;
+    dispatch(kmax_for(f->k), kVar, [&](auto KMAX, auto KM) {
+        k_probe<decltype(KMAX)::value, decltype(KM)::value>
+            <<<1, 64, 0, f->stream>>>(ks, 1, int(f->k), f->im, f->bitmap, st->dev, int(f->k));
+    });
+    CHECK_LAUNCH();
+    WAIT(f);
+    const uint8_t hit = *reinterpret_cast<volatile uint8_t*>(st->host);
+    if (hit > 1) return fail(PBF_ERR_HIP, "one-key probe: result byte not written");
+    *out = hit;
+    f->last_probe_mode = PBF_PROBE_DIRECT;
+    f->last_probe_detail = PBF_DETAIL_ONE_KEY;
     return PBF_OK;
 }
 
@@ -1199,7 +1502,7 @@ void* pbf_device_bitmap(pbf_filter_t* f) {
 }
 
 int pbf_set_build_mode(pbf_filter_t* f, int mode) {
-    if (!f) return fail(PBF_ERR_INVALID, "null filter handle");
+    LOCK(f);
     if (mode < PBF_BUILD_AUTO || mode > PBF_BUILD_TILED) return fail(PBF_ERR_INVALID, "bad build mode");
     if (mode == PBF_BUILD_TILED && (!f->tiled_ok || f->k > 32 || !part_fits(f->tm.nbuckets, f->k, false)))
         return fail(PBF_ERR_INVALID, "tiled build unsupported for this m / k");
@@ -1210,7 +1513,7 @@ int pbf_set_build_mode(pbf_filter_t* f, int mode) {
 int pbf_last_build_mode(pbf_filter_t* f) { return f ? f->last_mode : 0; }
 
 int pbf_set_probe_mode(pbf_filter_t* f, int mode) {
-    if (!f) return fail(PBF_ERR_INVALID, "null filter handle");
+    LOCK(f);
     if (mode < PBF_PROBE_AUTO || mode > PBF_PROBE_TILED) return fail(PBF_ERR_INVALID, "bad probe mode");
     if (mode == PBF_PROBE_TILED &&
         (!f->tiled_ok || f->k > 32 || f->tm.tb > kSlotShift || !part_fits(f->tm.nbuckets, f->k, true)))
@@ -1220,6 +1523,7 @@ int pbf_set_probe_mode(pbf_filter_t* f, int mode) {
 }
 
 int pbf_last_probe_mode(pbf_filter_t* f) { return f ? f->last_probe_mode : 0; }
+uint32_t pbf_last_probe_detail(pbf_filter_t* f) { return f ? f->last_probe_detail : 0; }
 
 int pbf_encode_data_blocks(int device, const uint8_t* keys, const uint64_t* key_offsets, const uint8_t* values,
                            const uint64_t* value_offsets, uint64_t n, const uint64_t* block_first,

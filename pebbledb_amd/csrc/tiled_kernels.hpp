@@ -494,13 +494,11 @@ __device__ __forceinline__ uint32_t r_quad(uint32_t rw, uint32_t r) {
 // region).  Each lane tests its 4 entries in the LDS tile; four ballots give every word's 32
 // result bits, stored by the word's first lane.  `expand` = the LDS budget allows a per-word
 // region id table (else a binary search over the word prefix).
-__global__ void __launch_bounds__(1024) k_tile_probe(TileMap tm, PartGeom pg, const uint32_t* __restrict__ regions,
-                                                     const uint32_t* __restrict__ fill,
-                                                     const uint32_t* __restrict__ bitmap, uint32_t* __restrict__ R,
-                                                     int expand) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+__device__ __forceinline__ void tile_probe_body(uint32_t* smem, uint32_t b, const TileMap& tm, const PartGeom& pg,
+                                                const uint32_t* __restrict__ regions, const uint32_t* __restrict__ fill,
+                                                const uint32_t* __restrict__ bitmap, uint32_t* __restrict__ R,
+                                                int expand) {
     const uint32_t B = tm.nbuckets, G = pg.G, cap = pg.cap, wpr = cap / 32;
-    const uint32_t b = blockIdx.x;
     const uint32_t W = 1u << (tm.tb - 5);
     uint32_t* tile = smem;          // W
     uint32_t* fills = tile + W;     // G
@@ -558,6 +556,31 @@ __global__ void __launch_bounds__(1024) k_tile_probe(TileMap tm, PartGeom pg, co
             }
         }
     }
+}
+
+__global__ void __launch_bounds__(1024) k_tile_probe(TileMap tm, PartGeom pg, const uint32_t* __restrict__ regions,
+                                                     const uint32_t* __restrict__ fill,
+                                                     const uint32_t* __restrict__ bitmap, uint32_t* __restrict__ R,
+                                                     int expand) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    tile_probe_body(smem, blockIdx.x, tm, pg, regions, fill, bitmap, R, expand);
+}
+
+// The tile test of a multi-filter probe in ONE launch: workgroup (tile b, filter f) for every
+// filter of the set.  Workgroups are dealt round-robin over the 8 XCDs in dispatch order (speed
+// only, never correctness), so block x = ((b / 8) * nf + f) * 8 + b % 8 puts the nf
+// workgroups of tile b on one XCD, dispatched together: they stream the same region entries
+// (g, b), g = 0..G-1, in the same order, and all but the first read them from that XCD's L2.
+__global__ void __launch_bounds__(1024) k_tile_probe_set(TileMap tm, PartGeom pg, const uint32_t* __restrict__ regions,
+                                                         const uint32_t* __restrict__ fill, ProbeSet ps,
+                                                         uint32_t* __restrict__ R, uint64_t r_stride, int expand) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    const uint32_t x = blockIdx.x, nf = ps.nf;
+    const uint32_t t = x >> 3;
+    const uint32_t f = t % nf;
+    const uint32_t b = (t / nf) * 8 + (x & 7);
+    if (b >= tm.nbuckets) return;
+    tile_probe_body(smem, b, tm, pg, regions, fill, ps.bm[f], R + f * r_stride, expand);
 }
 
 // Workgroup g owns keys [g*kpw, (g+1)*kpw) and regions (g, 0..B-1).  It reads each region once,

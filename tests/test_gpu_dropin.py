@@ -1,0 +1,166 @@
+"""The drop-in surface under the reference's calling patterns (runs on an MI355X, `-m gpu`):
+per-key may_contain (LsmStorage.get, src/lsm_storage.py:165,175) through the one-key launch,
+reader threads sharing one filter without a lock (lsm_storage.py:153-179), host staging in
+chunks smaller than one hit-mask byte's worth of keys, and the pooled working memory."""
+import os
+import subprocess
+import sys
+import textwrap
+import threading
+
+import numpy as np
+import pytest
+
+from pebbledb_amd import BloomFilter, PackedKeys, may_contain_multi
+from pebbledb_amd import _native
+from pebbledb_amd.keys import splitmix_hex_keys, varlen_keys
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _strs(pk: PackedKeys) -> list[str]:
+    return [pk.key(i).decode("utf-8") for i in range(pk.n)]
+
+
+def test_one_key_may_contain_matches_oracle(oracle):
+    """pbf_may_contain (one launch, key via mapped pinned memory) == the oracle, over fixed,
+    variable-length, empty, non-ASCII and > 4096-byte keys, for power-of-two and floor-mod m."""
+    d, o = varlen_keys(5, 0, 3000)
+    members = PackedKeys(d, 3000, offsets=o)
+    extra = ["", "é", "ключ", "🔑" * 3, "x" * 5000, "y" * 4096, "z" * 4097]
+    keys = _strs(members) + extra
+    probes = keys + [s + "!" for s in keys[:1500]] + ["absent-%d" % i for i in range(500)]
+    for nb, k in ((2 ** 14, 6), (100_003, 7), (777, 3), (64, 40)):
+        bf = BloomFilter(nb, k)
+        bf.add_many(keys)
+        want = oracle.build(nb, k, PackedKeys.from_strs(keys))
+        assert bf.bitmap() == want.tobytes()
+        want_hm = np.unpackbits(oracle.probe(want, k, PackedKeys.from_strs(probes)), bitorder="little")
+        got = [bf.may_contain(s) for s in probes]
+        assert got == [bool(x) for x in want_hm[:len(probes)]], (nb, k)
+        assert bf.last_probe_detail & _native.PBF_DETAIL_ONE_KEY or len(probes[-1]) > 4096
+
+
+def test_reader_threads_share_one_filter(oracle):
+    """Eight threads call may_contain / may_contain_many on ONE filter at once (the reference's
+    reader threads, no lock) while a ninth adds keys to another filter: every answer equals the
+    oracle's."""
+    n = 50_000
+    pk = PackedKeys.fixed(splitmix_hex_keys(11, 0, n))
+    bf = BloomFilter(2 ** 16, 5)
+    bf.add_many(pk)
+    want = oracle.build(2 ** 16, 5, pk)
+    q = PackedKeys.fixed(splitmix_hex_keys(11, n // 2, n))
+    want_hm = oracle.probe(want, 5, q)
+    want_bits = np.unpackbits(want_hm, bitorder="little")[:n]
+    qs = _strs(q)
+    errors = []
+
+    def reader(t):
+        try:
+            for rep in range(3):
+                if (t + rep) % 2:
+                    got = bf.may_contain_many(q, packed=True)
+                    if not np.array_equal(got, want_hm):
+                        errors.append(("batch", t))
+                else:
+                    for i in range(t, n, 97):
+                        if bf.may_contain(qs[i]) != bool(want_bits[i]):
+                            errors.append(("key", t, i))
+                            break
+        except Exception as e:  # pragma: no cover - reported below
+            errors.append(("exc", t, repr(e)))
+
+    other = BloomFilter(2 ** 16, 5)
+
+    def writer():
+        for i in range(0, n, 5000):
+            other.add_many(PackedKeys.fixed(splitmix_hex_keys(11, i, 5000)))
+
+    th = [threading.Thread(target=reader, args=(t,)) for t in range(8)] + [threading.Thread(target=writer)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    assert not errors, errors[:5]
+    assert other.bitmap() == want.tobytes()
+    # concurrent add() buffering on one filter from several threads
+    shared = BloomFilter(2 ** 16, 5)
+    strs = _strs(pk)
+
+    def adder(t):
+        for s in strs[t::4]:
+            shared.add(s)
+
+    th = [threading.Thread(target=adder, args=(t,)) for t in range(4)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    assert shared.bitmap() == want.tobytes()
+
+
+def test_stage_chunks_smaller_than_a_hitmask_byte(oracle):
+    """PBF_STAGE_BYTES smaller than 64 keys' worth of bytes: every host-staged chunk but the last
+    still holds a multiple of 64 keys, so hit-mask bytes never straddle chunks (single and
+    multi-filter probes; fixed and variable-length keys)."""
+    code = textwrap.dedent("""
+        import numpy as np, sys
+        sys.path.insert(0, '.')
+        from pebbledb_amd import BloomFilter, PackedKeys, may_contain_multi
+        from pebbledb_amd.keys import splitmix_hex_keys, varlen_keys
+        from oracle.oracle import COracle
+        o = COracle()
+        fx = PackedKeys.fixed(splitmix_hex_keys(3, 0, 3001))
+        d, off = varlen_keys(3, 0, 3001)
+        vr = PackedKeys(d, 3001, offsets=off)
+        for pk in (fx, vr):
+            fs = []
+            for mode in (1, 2):
+                bf = BloomFilter(50000, 6); bf.set_build_mode(mode); bf.add_many(pk)
+                want = o.build(50000, 6, pk)
+                assert bf.bitmap() == want.tobytes()
+                for pm in (1, 2):
+                    bf.set_probe_mode(pm)
+                    assert np.array_equal(bf.may_contain_many(pk, packed=True), o.probe(want, 6, pk))
+                fs.append(bf)
+            m = may_contain_multi(fs, pk)
+            assert np.array_equal(m[0], o.probe(want, 6, pk)) and np.array_equal(m[1], m[0])
+        print('ok')
+    """)
+    env = dict(os.environ, PBF_STAGE_BYTES="200")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=600, cwd=REPO)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
+
+
+def test_scratch_is_pooled_not_per_filter(oracle):
+    """Working memory is a per-device pool: building and probing many filters leaves the pool at
+    the size of the largest single pipeline (not growing with the number of filters), each
+    filter holding only its bitmap; pbf_trim releases the pool and later calls still work."""
+    L = _native.lib()
+
+    def pool_bytes():
+        v = _native._u64(0)
+        _native.check(L.pbf_scratch_bytes(0, __import__("ctypes").byref(v)), "scratch")
+        return v.value
+
+    pk = PackedKeys.fixed(splitmix_hex_keys(4, 0, 300_000))
+    want = oracle.build(2 ** 20, 6, pk)
+    fs = []
+    sizes = []
+    for i in range(12):
+        bf = BloomFilter(2 ** 20, 6)
+        bf.set_build_mode(2)
+        bf.set_probe_mode(2)
+        bf.add_many(pk)
+        assert np.array_equal(bf.may_contain_many(pk, packed=True)[:1000], np.full(1000, 0xFF, np.uint8))
+        fs.append(bf)
+        sizes.append(pool_bytes())
+    assert max(sizes[4:]) <= max(sizes[:4]), sizes  # bounded by the pipeline, not by the filter count
+    _native.check(L.pbf_trim(0), "trim")
+    assert pool_bytes() == 0
+    for bf in fs[:3]:
+        assert bf.bitmap() == want.tobytes()
+        assert bf.may_contain_many(pk).all()

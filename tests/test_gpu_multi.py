@@ -132,3 +132,96 @@ def test_multi_device_c5_shape(oracle):
         assert bits[f * per:(f + 1) * per].all(), f  # its own members
         want = oracle.build(nb, k, PackedKeys.fixed(splitmix_hex_keys(SEED, f * n_per, n_per)), omp=True)
         assert np.array_equal(h[:25_000], oracle.probe(want, k, PackedKeys.fixed(qh), omp=True)), f
+
+
+# ---------------------------------------------------------------- C5 as benchmarked
+def _c5_filters(oracle, nf, n_per, nb=2 ** 27, k=6):
+    """nf SSTable filters of the C5 geometry (m = 2^30, k = 6), filter f built on device from
+    keys [f*n_per, (f+1)*n_per); plus the oracle's bitmaps (OpenMP C restatement)."""
+    keys = _dev_hex(SEED, 0, nf * n_per)
+    fs = []
+    for f in range(nf):
+        bf = BloomFilter(nb, k)
+        bf.add_device_fixed(keys.data_ptr() + f * n_per * 16, 16, n_per)
+        fs.append(bf)
+    for bf in fs:
+        bf.sync()
+    host = keys.cpu().numpy().reshape(-1, 16)
+    del keys
+    want = [oracle.build(nb, k, PackedKeys.fixed(host[f * n_per:(f + 1) * n_per]), omp=True) for f in range(nf)]
+    for f, bf in enumerate(fs):
+        assert bf.bitmap() == want[f].tobytes(), f
+    return fs, want
+
+
+def _c5_probe_and_check(oracle, fs, want, q, nq, k=6, sample=(0, 1_000_000)):
+    """One device multi-probe of q (nq 16-B keys) against fs; every filter's hit mask equals
+    its own single-filter probe over the whole batch and the oracle's on [sample)."""
+    nf = len(fs)
+    hms = [torch.zeros((nq + 7) // 8, dtype=torch.uint8, device="cuda") for _ in range(nf)]
+    torch.cuda.synchronize()
+    probe_multi_device(fs, q.data_ptr(), nq, [h.data_ptr() for h in hms], key_len=16)
+    fs[0].sync()
+    detail = fs[0].last_probe_detail
+    got = [h.cpu().numpy() for h in hms]
+    single = torch.zeros((nq + 7) // 8, dtype=torch.uint8, device="cuda")
+    a, b = sample
+    qh = PackedKeys.fixed(q[a * 16:b * 16].cpu().numpy().reshape(-1, 16))
+    for f, bf in enumerate(fs):
+        single.zero_()
+        torch.cuda.synchronize()
+        bf.probe_device_fixed(q.data_ptr(), 16, nq, single.data_ptr())
+        bf.sync()
+        assert np.array_equal(got[f], single.cpu().numpy()), f
+        assert np.array_equal(got[f][a // 8:b // 8], oracle.probe(want[f], k, qh, omp=True)[: (b - a) // 8]), f
+    return got, detail
+
+
+@pytest.mark.timeout(600)
+def test_c5_full_geometry_fused_ring_gather(oracle):
+    """BASELINE.json configs[4] on one GPU as bench.py runs it: 8 filters (nb_bytes = 2^27,
+    k = 6, 10M keys each) and one device multi-probe of 20M + 37 keys (half members spread over
+    the 8 SSTables, half absent): B = 1024 tiles takes the RING partition, the XCD-aware fused
+    tile test and ONE fused k_gather_ring<8> (checked via last_probe_detail).  Every filter's
+    mask == its single probe over the whole batch == the oracle on a 1M-key sample; members all
+    hit; the false-positive count is at the theoretical rate."""
+    nf, n_per = 8, 10_000_000
+    fs, want = _c5_filters(oracle, nf, n_per)
+    nq = 20_000_037
+    half = nq // 2
+    per = half // nf
+    q = torch.empty(nq * 16, dtype=torch.uint8, device="cuda")
+    for f in range(nf):
+        cnt = per if f < nf - 1 else half - (nf - 1) * per
+        _dev_hex(SEED, f * n_per, cnt, q, f * per)
+    _dev_hex(SEED, nf * n_per, nq - half, q, half)
+    got, detail = _c5_probe_and_check(oracle, fs, want, q, nq, sample=(half - 500_000, half + 500_000))
+    assert detail & _native.PBF_DETAIL_RING and detail >> 8 == nf, hex(detail)
+    for f in range(nf):
+        bits = np.unpackbits(got[f], bitorder="little")[:nq]
+        cnt = per if f < nf - 1 else half - (nf - 1) * per
+        assert bits[f * per:f * per + cnt].all(), f
+        fill = fs[f].popcount() / (8 * 2 ** 27)
+        fp = int(bits[half:].sum())
+        assert fp <= 3 * (nq - half) * fill ** 6 + 20, (f, fp)
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("nf", [2, 5])
+def test_c5_geometry_small_sets_ragged_and_spills(oracle, nf):
+    """The same ring + fused path with 2 and 5 filters, a ragged batch, and keys repeated 60k and
+    50k times so the multi-filter partition's rings and regions overflow (spilled positions are
+    tested against every filter's bitmap inside the partition)."""
+    n_per = 2_000_000
+    fs, want = _c5_filters(oracle, nf, n_per)
+    base = nf * n_per // 2 + 3
+    rep_member = np.repeat(splitmix_hex_keys(SEED, 5, 1), 60_000, axis=0)           # member of filter 0
+    rep_absent = np.repeat(splitmix_hex_keys(SEED + 1, 0, 1), 50_000, axis=0)
+    qh = np.concatenate([splitmix_hex_keys(SEED, 0, base), rep_member,
+                         splitmix_hex_keys(SEED, nf * n_per, 777_777), rep_absent])
+    nq = len(qh)
+    q = torch.from_numpy(qh.reshape(-1)).cuda()
+    got, detail = _c5_probe_and_check(oracle, fs, want, q, nq, sample=(0, nq // 8 * 8))
+    assert detail & _native.PBF_DETAIL_RING and detail >> 8 == nf, hex(detail)
+    b0 = np.unpackbits(got[0], bitorder="little")[:nq]
+    assert b0[base:base + 60_000].all()  # the repeated member hits filter 0 every time
