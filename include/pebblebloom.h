@@ -163,6 +163,18 @@ int pbf_encode_data_blocks(int device, const uint8_t* keys, const uint64_t* key_
                            const uint64_t* value_offsets, uint64_t n, const uint64_t* block_first,
                            const uint64_t* block_out, uint64_t nblocks, uint8_t* out, int on_device);
 
+/* The level key-range pre-check of LsmStorage.get (src/lsm_storage.py:171-175) for a batch:
+ * out[t * ceil(n/8) + i/8] bit (i & 7) = (first_t <= key_i <= last_t), Python str order =
+ * bytewise lexicographic order of the UTF-8 keys.  Bounds are 2*ntables byte strings
+ * (first_0, last_0, first_1, last_1, ...): bound j = bounds[bound_offsets[j] - bound_offsets[0],
+ * bound_offsets[j+1] - bound_offsets[0]).  Keys as in pbf_probe (offsets != NULL) or fixed
+ * key_len (offsets == NULL).  The mask layout is the hit-mask layout, so it ANDs directly with
+ * the table's filter hit mask.  on_device = 0: host pointers, synchronous; on_device = 1:
+ * device pointers (bound_offsets is read back first), asynchronous on `stream`. */
+int pbf_key_range_mask(int device, void* stream, const uint8_t* keys, const uint64_t* offsets, uint32_t key_len,
+                       uint64_t n, const uint8_t* bounds, const uint64_t* bound_offsets, uint32_t ntables, uint8_t* out,
+                       int on_device);
+
 /* Synthetic keys straight into device memory (bench / tests; definitions in
  * pebbledb_amd/keys.py): 16 hex chars of splitmix64(seed + start + i), and the variable-length
  * 8..64-byte family (offsets must already hold the n+1 offsets, relative to offsets[0]). */

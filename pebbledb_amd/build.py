@@ -11,7 +11,7 @@ CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libpebblebloom.so")
 SOURCES = [os.path.join(CSRC, "pebblebloom.hip")]
 DEPS = SOURCES + [os.path.join(CSRC, f) for f in ("bloom_kernels.hpp", "murmur_device.hpp", "tiled_kernels.hpp", "ring_kernels.hpp",
-                                                "sstable_kernels.hpp")] + [
+                                                "sstable_kernels.hpp", "lsm_kernels.hpp")] + [
     os.path.join(REPO, "include", "pebblebloom.h")]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("PBF_OFFLOAD_ARCH", "gfx950")

@@ -27,6 +27,7 @@
 #include "tiled_kernels.hpp"
 #include "ring_kernels.hpp"
 #include "sstable_kernels.hpp"
+#include "lsm_kernels.hpp"
 
 using namespace pbf;
 
@@ -1586,6 +1587,94 @@ int pbf_encode_data_blocks(int device, const uint8_t* keys, const uint64_t* key_
     if (!on_device) HIP_TRY(hipMemcpyAsync(out, dout, out_bytes, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     if (err) return fail(PBF_ERR_INVALID, std::to_string(err) + " block(s) exceed 65536 data bytes; not written");
+    return PBF_OK;
+}
+
+int pbf_key_range_mask(int device, void* stream, const uint8_t* keys, const uint64_t* offsets, uint32_t key_len,
+                       uint64_t n, const uint8_t* bounds, const uint64_t* bound_offsets, uint32_t ntables, uint8_t* out,
+                       int on_device) {
+    if (n == 0 || ntables == 0) return PBF_OK;
+    if (!bound_offsets || !out || (!keys && !offsets)) return fail(PBF_ERR_INVALID, "null pointer");
+    HIP_TRY(hipSetDevice(device));
+    const uint64_t stride = (n + 7) / 8;
+    // table groups whose bounds fit the LDS stage (host-side sizes: the offsets are read on the
+    // host for the host path, copied back first for the device path)
+    std::vector<uint64_t> bo(2 * size_t(ntables) + 1);
+    if (on_device)
+        HIP_TRY(hipMemcpy(bo.data(), bound_offsets, bo.size() * 8, hipMemcpyDeviceToHost));
+    else
+        std::memcpy(bo.data(), bound_offsets, bo.size() * 8);
+    std::vector<std::pair<uint32_t, uint32_t>> groups;  // (t0, nt, words)
+    std::vector<uint32_t> gwords;
+    {
+        uint32_t t0 = 0, w = 0;
+        for (uint32_t t = 0; t < ntables; ++t) {
+            uint32_t tw = 0;
+            for (int e = 0; e < 2; ++e) {
+                const uint64_t bl = bo[2 * t + e + 1] - bo[2 * t + e];
+                if (bl > 64 * 1024) return fail(PBF_ERR_INVALID, "an SSTable bound key is longer than 65536 bytes");
+                tw += uint32_t((bl + 3) / 4);
+            }
+            const uint32_t nt = t - t0 + 1;
+            if (t > t0 && (size_t(w + tw) * 4 + size_t(4 * nt + 1) * 4 > kRangeLdsBytes || nt > 4096)) {
+                groups.emplace_back(t0, t - t0);
+                gwords.push_back(w);
+                t0 = t;
+                w = 0;
+            }
+            w += tw;
+        }
+        groups.emplace_back(t0, ntables - t0);
+        gwords.push_back(w);
+    }
+    EncodeCtx& c = encode_ctx(device);
+    std::lock_guard<std::mutex> lock(c.mu);
+    if (!c.stream) HIP_TRY(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
+    hipStream_t s = on_device ? static_cast<hipStream_t>(stream) : c.stream;
+    const uint8_t *dk = keys, *db = bounds;
+    const uint64_t *dko = offsets, *dbo = bound_offsets;
+    uint8_t* dout = out;
+    if (!on_device) {
+        const uint64_t kb = offsets ? offsets[n] - offsets[0] : n * uint64_t(key_len);
+        const uint64_t bb = bo[2 * size_t(ntables)] - bo[0];
+        HIP_TRY(c.keys.ensure(kb + 16));
+        HIP_TRY(c.vals.ensure(bb + 16));
+        HIP_TRY(c.offs.ensure(((offsets ? n + 1 : 0) + bo.size()) * 8));
+        HIP_TRY(c.out.ensure(stride * ntables + 16));
+        auto* o = static_cast<uint64_t*>(c.offs.p);
+        if (kb) HIP_TRY(hipMemcpyAsync(c.keys.p, keys + (offsets ? offsets[0] : 0), kb, hipMemcpyHostToDevice, s));
+        if (bb) HIP_TRY(hipMemcpyAsync(c.vals.p, bounds + bo[0], bb, hipMemcpyHostToDevice, s));
+        if (offsets) HIP_TRY(hipMemcpyAsync(o, offsets, (n + 1) * 8, hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemcpyAsync(o + (offsets ? n + 1 : 0), bo.data(), bo.size() * 8, hipMemcpyHostToDevice, s));
+        dk = static_cast<const uint8_t*>(c.keys.p);
+        db = static_cast<const uint8_t*>(c.vals.p);
+        dko = offsets ? o : nullptr;
+        dbo = o + (offsets ? n + 1 : 0);
+        dout = static_cast<uint8_t*>(c.out.p);
+    }
+    const Batch b = make_batch(dk, dko, key_len, n);
+    const uint32_t grid = grid_for(n, 256, 1024);
+    for (size_t gi = 0; gi < groups.size(); ++gi) {
+        RangeSet rs{};
+        rs.bytes = db;
+        rs.offsets = dbo;
+        rs.t0 = groups[gi].first;
+        rs.nt = groups[gi].second;
+        rs.lds_words = gwords[gi];
+        const size_t lds = (size_t(4 * rs.nt + 1) + rs.lds_words) * 4;
+        if (b.km == kVar) {
+            HIP_TRY(allow_lds(k_range_mask<kVar>, lds));
+            k_range_mask<kVar><<<grid, 256, lds, s>>>(b.ks, n, rs, dout, stride);
+        } else {
+            HIP_TRY(allow_lds(k_range_mask<kFixedN>, lds));
+            k_range_mask<kFixedN><<<grid, 256, lds, s>>>(b.ks, n, rs, dout, stride);
+        }
+        CHECK_LAUNCH();
+    }
+    if (!on_device) {
+        HIP_TRY(hipMemcpyAsync(out, dout, stride * ntables, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+    }
     return PBF_OK;
 }
 

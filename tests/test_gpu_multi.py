@@ -166,6 +166,7 @@ def _c5_probe_and_check(oracle, fs, want, q, nq, k=6, sample=(0, 1_000_000)):
     got = [h.cpu().numpy() for h in hms]
     single = torch.zeros((nq + 7) // 8, dtype=torch.uint8, device="cuda")
     a, b = sample
+    a, b = a - a % 8, b - b % 8  # whole hit-mask bytes
     qh = PackedKeys.fixed(q[a * 16:b * 16].cpu().numpy().reshape(-1, 16))
     for f, bf in enumerate(fs):
         single.zero_()

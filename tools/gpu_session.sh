@@ -103,7 +103,7 @@ for step in "$@"; do
            for t in 0 16; do PBF_TDEPTH=$t run wrreq_$t 300 rocprofv3 --pmc TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum --output-format csv -d gpurun_out/wrreq_$t -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-host-inclusive; done ;;
     chunks) for c in ${PBF_CHUNKS:-2000000 4000000 6000000 10000000}; do PBF_PROBE_CHUNK=$c run chunk_$c 300 python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-host-inclusive; done
             run chunk_none 300 python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-host-inclusive ;;
-    pytest_new) run pytest_new 900 python -u -m pytest tests/test_gpu_multi.py tests/test_gpu_dropin.py tests/test_gpu_distributed.py -m gpu -x -v -rf --timeout 600 --timeout-method thread ;;
+    pytest_new) run pytest_new 900 python -u -m pytest tests/test_gpu_multi.py tests/test_gpu_dropin.py tests/test_gpu_distributed.py tests/test_gpu_lsm_get.py -m gpu -x -v -rf --timeout 600 --timeout-method thread ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
