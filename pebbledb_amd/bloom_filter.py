@@ -31,7 +31,7 @@ from typing import Iterable, Optional
 import numpy as np
 
 from . import _native
-from .keys import PackedKeys
+from .keys import PackedKeys, PackedRecords
 
 _PENDING_FLUSH = 1 << 16
 _default_device = int(os.environ.get("PBF_DEVICE", os.environ.get("LOCAL_RANK", "0")))
@@ -219,6 +219,8 @@ class BloomFilter:
     @classmethod
     def build_from_keys_and_fp_rate(cls, keys, fp_rate: float, device: Optional[int] = None) -> "BloomFilter":
         """bloom_filter.py:92-119 — same sizing expression order; one batched device build."""
+        if isinstance(keys, PackedRecords):
+            keys = keys.keys
         n = keys.n if isinstance(keys, PackedKeys) else len(keys)
         m = (-n * log(fp_rate)) / (log(2) ** 2)
         k = (m / n) * log(2)
@@ -228,8 +230,16 @@ class BloomFilter:
 
     # ------------------------------------------------------------------ batch extensions
     def add_many(self, keys) -> None:
-        """add() for every key of `keys` (list[str] / iterable of str / PackedKeys)."""
-        pk = keys if isinstance(keys, PackedKeys) else PackedKeys.from_strs(list(keys))
+        """add() for every key of `keys` (list[str] / any iterable of str or records /
+        PackedKeys / PackedRecords); iterables are packed as they are drained."""
+        if isinstance(keys, PackedRecords):
+            keys = keys.keys
+        if isinstance(keys, PackedKeys):
+            pk = keys
+        elif isinstance(keys, list):
+            pk = PackedKeys.from_strs(keys)
+        else:
+            pk = PackedKeys.from_iter(keys)
         self._add_packed(pk)
 
     def may_contain_many(self, keys, packed: bool = False) -> np.ndarray:

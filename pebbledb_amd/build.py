@@ -51,6 +51,29 @@ def build_lib(force: bool = False, verbose: bool = True, out: str = LIB, defines
     return out
 
 
+INGEST_SRC = os.path.join(CSRC, "ingest.c")
+
+
+def ingest_path() -> str:
+    import sysconfig
+    return os.path.join(PKG, "_pebbleingest" + sysconfig.get_config_var("EXT_SUFFIX"))
+
+
+def build_ingest(force: bool = False, verbose: bool = True) -> str:
+    """The host-side packed-ingestion extension (csrc/ingest.c, CPython C API, gcc)."""
+    import sysconfig
+    out = ingest_path()
+    if not force and os.path.exists(out) and os.path.getmtime(out) >= os.path.getmtime(INGEST_SRC):
+        return out
+    cmd = [os.environ.get("CC", "gcc"), "-O2", "-fPIC", "-shared", "-Wall", "-Wextra", "-Wno-missing-field-initializers",
+           "-Wno-unused-parameter", "-I", sysconfig.get_paths()["include"], "-o", out + ".tmp", INGEST_SRC]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(out + ".tmp", out)
+    return out
+
+
 if __name__ == "__main__":
     # python -m pebbledb_amd.build [--force] [--out PATH -DNAME ...]
     args = sys.argv[1:]

@@ -8,7 +8,8 @@ batch of keys is either
   ``bytes[offsets[i]:offsets[i+1]]``).
 
 Synthetic workloads — the same definitions are implemented by the device
-generators in csrc/keygen.hip and checked against these in tests:
+generators ``k_gen_splitmix_hex`` / ``k_gen_varlen`` (csrc/bloom_kernels.hpp) and checked
+against these in tests:
 
 * ``splitmix_hex``: key ``i`` = 16 lowercase hex chars of ``splitmix64(seed + i)``.
 * ``varlen``: ``h = splitmix64((seed << 32) + i)``; length ``8 + h % 57`` (8..64 bytes);
@@ -127,7 +128,67 @@ class PackedKeys:
         a = np.ascontiguousarray(arr2d, dtype=np.uint8)
         return cls(a.reshape(-1), a.shape[0], key_len=a.shape[1])
 
+    @classmethod
+    def from_iter(cls, keys) -> "PackedKeys":
+        """Pack an iterable of str / bytes keys (or records: (key, value) pairs or objects with
+        .key) as it is drained, in one C loop (csrc/ingest.c) — no list[str] materialised."""
+        kb, ko, _, _, n, _, lo, hi = _ingest().pack_keys(keys)
+        return cls._from_packed(kb, ko, n, lo, hi)
+
+    @classmethod
+    def _from_packed(cls, kb, ko, n, lo, hi) -> "PackedKeys":
+        data = np.frombuffer(kb, dtype=np.uint8) if len(kb) else np.zeros(0, np.uint8)
+        if n and lo == hi and lo > 0:
+            return cls(data, n, key_len=int(lo))
+        return cls(data, n, key_len=0, offsets=np.frombuffer(ko, dtype=np.uint64))
+
     def key(self, i: int) -> bytes:
         if self.key_len > 0:
             return self.data[i * self.key_len:(i + 1) * self.key_len].tobytes()
         return self.data[int(self.offsets[i]):int(self.offsets[i + 1])].tobytes()
+
+
+def _ingest():
+    """The packed-ingestion extension (built by pebbledb_amd/build.py; host code, no GPU)."""
+    from . import _pebbleingest
+    return _pebbleingest
+
+
+class PackedRecords:
+    """A flushed / compacted run of records in the boundary layout: keys (PackedKeys) plus value
+    bytes and u64 value offsets[n+1] — what SSTableBuilder.add accumulates record by record
+    (src/sstable.py:224-244), packed straight from the iterator that yields them
+    (MemTableIterator / MergingIterator, src/iterators.py:24-55,144-190)."""
+
+    __slots__ = ("keys", "values", "value_offsets", "n", "ascii")
+
+    def __init__(self, keys: PackedKeys, values: np.ndarray, value_offsets: np.ndarray, ascii: bool = False):
+        self.keys = keys
+        self.values = values
+        self.value_offsets = value_offsets
+        self.n = keys.n
+        self.ascii = bool(ascii)
+        if len(value_offsets) != self.n + 1:
+            raise ValueError("value offsets must have n+1 entries")
+
+    @classmethod
+    def from_iter(cls, records) -> "PackedRecords":
+        """Drain `records` — Record objects (.key str, .value bytes), (key, value) pairs — in one
+        C loop into packed key / value buffers."""
+        kb, ko, vb, vo, n, ascii, lo, hi = _ingest().pack_records(records)
+        keys = PackedKeys._from_packed(kb, ko, n, lo, hi)
+        values = np.frombuffer(vb, dtype=np.uint8) if len(vb) else np.zeros(0, np.uint8)
+        return cls(keys, values, np.frombuffer(vo, dtype=np.uint64), ascii=bool(ascii))
+
+    @classmethod
+    def from_encoded(cls, encoded) -> "PackedRecords":
+        """Drain encoded records — the bytes the memtable stores (memtable.map values,
+        Record.to_bytes, src/record.py:66-72) — split exactly as Record._from_bytes does
+        (record.py:77-88), in one C loop: no Record objects are created."""
+        kb, ko, vb, vo, n, ascii, lo, hi = _ingest().pack_encoded(encoded)
+        keys = PackedKeys._from_packed(kb, ko, n, lo, hi)
+        values = np.frombuffer(vb, dtype=np.uint8) if len(vb) else np.zeros(0, np.uint8)
+        return cls(keys, values, np.frombuffer(vo, dtype=np.uint64), ascii=bool(ascii))
+
+    def key_str(self, i: int) -> str:
+        return self.keys.key(i).decode("utf-8")

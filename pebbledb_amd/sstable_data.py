@@ -26,7 +26,7 @@ import struct
 import numpy as np
 
 from . import _native
-from .keys import PackedKeys
+from .keys import PackedKeys, PackedRecords
 
 BLOCK_SIZE = 65_536  # SSTableBuilder default (sstable.py:215)
 RECORD_HEADER = 8    # two i32 sizes (record.py:66-72)
@@ -93,11 +93,13 @@ def encode_data_blocks(pk: PackedKeys, vals: np.ndarray, vo: np.ndarray, block_f
     return out
 
 
-def meta_blocks(keys: list[str], block_first: np.ndarray, block_out: np.ndarray) -> tuple[bytes, list]:
-    """MetaBlock.to_bytes of every block (blocks.py:126-133) and the (first, last, offset) list."""
+def meta_blocks(keys, block_first: np.ndarray, block_out: np.ndarray) -> tuple[bytes, list]:
+    """MetaBlock.to_bytes of every block (blocks.py:126-133) and the (first, last, offset) list.
+    `keys`: list[str] or PackedKeys (only the blocks' first / last keys are decoded)."""
+    key = (lambda i: keys.key(i).decode("utf-8")) if isinstance(keys, PackedKeys) else keys.__getitem__
     parts, metas = [], []
     for b in range(len(block_first) - 1):
-        first, last = keys[int(block_first[b])], keys[int(block_first[b + 1]) - 1]
+        first, last = key(int(block_first[b])), key(int(block_first[b + 1]) - 1)
         off = int(block_out[b])
         metas.append((first, last, off))
         parts.append(struct.pack("H", len(first)) + first.encode("utf-8") + struct.pack("H", len(last)) +
@@ -105,20 +107,29 @@ def meta_blocks(keys: list[str], block_first: np.ndarray, block_out: np.ndarray)
     return b"".join(parts), metas
 
 
-def build_sstable(keys, values, block_size: int = BLOCK_SIZE, fp_rate: float = 0.001, device=None):
+def build_sstable(keys, values=None, block_size: int = BLOCK_SIZE, fp_rate: float = 0.001, device=None):
     """The bytes SSTableBuilder(block_size=block_size) writes after add(k, v) for every record
-    and build() (sstable.py:270-288), plus the meta blocks and the device BloomFilter."""
+    and build() (sstable.py:270-288), plus the meta blocks and the device BloomFilter.
+
+    `keys` is either a PackedRecords (values None) — e.g. ``PackedRecords.from_iter(
+    MemTableIterator(memtable))``, the flush path with no per-record Python — or list[str] with
+    `values` list[bytes]."""
     from .bloom_filter import BloomFilter, _default_device
     from .sstable_bloom import encode_sstable
 
     dev = _default_device if device is None else int(device)
-    keys = keys if isinstance(keys, list) else list(keys)
-    pk = PackedKeys.from_strs(keys)
-    vals, vo = pack_values(values)
+    if isinstance(keys, PackedRecords):
+        if values is not None:
+            raise ValueError("PackedRecords carries its values")
+        pk, vals, vo = keys.keys, keys.values, keys.value_offsets
+    else:
+        keys = keys if isinstance(keys, list) else list(keys)
+        pk = PackedKeys.from_strs(keys)
+        vals, vo = pack_values(values)
     if len(vo) - 1 != pk.n:
         raise ValueError("keys and values differ in length")
     bf_first, bo = plan_blocks(key_offsets(pk), vo, block_size)
     data = encode_data_blocks(pk, vals, vo, bf_first, bo, dev)
-    meta, metas = meta_blocks(keys, bf_first, bo)
+    meta, metas = meta_blocks(keys if isinstance(keys, list) else pk, bf_first, bo)
     bloom = BloomFilter.build_from_keys_and_fp_rate(pk, fp_rate, device=dev)
     return encode_sstable(memoryview(data), meta, bloom), metas, bloom

@@ -9,7 +9,7 @@ import pytest
 
 from oracle import sstable_oracle as so
 from pebbledb_amd import _native
-from pebbledb_amd.keys import PackedKeys
+from pebbledb_amd.keys import PackedKeys, PackedRecords
 from pebbledb_amd.sstable_data import (build_sstable, encode_data_blocks, key_offsets, pack_values,
                                        plan_blocks)
 
@@ -25,6 +25,32 @@ def test_device_sstable_equals_reference_file(case):
     assert len(f) == case["file_len"]
     assert hashlib.sha256(bytes(f)).hexdigest() == case["file_sha256"]
     assert [m[2] for m in metas] == [m["offset"] for m in case["meta_blocks"]]
+
+
+@pytest.mark.parametrize("case", CASES, ids=[c["name"] for c in CASES])
+def test_packed_records_flush_equals_reference_file(case):
+    """The flush without list[str]: records packed as the iterator yields them (csrc/ingest.c)
+    give the same file bytes as the real reference's SSTableBuilder (sstable.py:224-288)."""
+    import struct
+
+    class Rec:
+        __slots__ = ("key", "value")
+
+        def __init__(self, k, v):
+            self.key, self.value = k, v
+
+    srcs = [PackedRecords.from_iter(zip(case["_keys"], case["_vals"])),
+            PackedRecords.from_iter(Rec(k, v) for k, v in zip(case["_keys"], case["_vals"]))]
+    if all(k.isascii() for k in case["_keys"]):  # encoded records split as Record._from_bytes does
+        srcs.append(PackedRecords.from_encoded(
+            [struct.pack("i", len(k)) + k.encode() + struct.pack("i", len(v)) + v
+             for k, v in zip(case["_keys"], case["_vals"])]))
+    for pr in srcs:
+        f, metas, bloom = build_sstable(pr, block_size=case["block_size"])
+        assert len(f) == case["file_len"]
+        assert hashlib.sha256(bytes(f)).hexdigest() == case["file_sha256"]
+        assert [m[2] for m in metas] == [m["offset"] for m in case["meta_blocks"]]
+        assert [(m[0], m[1]) for m in metas] == [(m["first_key"], m["last_key"]) for m in case["meta_blocks"]]
 
 
 def _random_records(rng, n, maxk, maxv, unicode_every=0):
