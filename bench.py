@@ -182,6 +182,50 @@ def host_inclusive(bf, keys, n, nb_bytes, L, torch, np, reps=3):
     }
 
 
+def dropin_latency(device, reps=2000):
+    """Per-call latency of the drop-in class at C1 size (BASELINE configs[0]: 1k 16-B keys,
+    m = 8192, k = 4) as pebbledb calls it — add per key then a read (SSTableBuilder.build,
+    sstable.py:274), may_contain per key (LsmStorage.get, lsm_storage.py:165,175), to_bytes
+    (sstable.py:82) — beside the reference algorithm (BigIntBloomPort, Python big-int bitmap)."""
+    from oracle.oracle import BigIntBloomPort
+    from pebbledb_amd import BloomFilter
+    from pebbledb_amd.keys import splitmix_hex_keys_str
+    keys = splitmix_hex_keys_str(SEED, 0, 1000)
+    probes = splitmix_hex_keys_str(SEED, 500, 1000)
+    out = {}
+    for name, cls in (("pebbledb_amd", BloomFilter), ("reference_port", BigIntBloomPort)):
+        kw = {"device": device} if cls is BloomFilter else {}
+        bf = cls(1024, 4, **kw)
+        t0 = time.perf_counter()
+        for k in keys:
+            bf.add(k)
+        blob = bf.to_bytes()  # the first read sends the buffered adds (one batched build)
+        t_add = time.perf_counter() - t0
+        for k in probes[:50]:
+            bf.may_contain(k)
+        t0 = time.perf_counter()
+        hits = 0
+        for i in range(reps):
+            hits += bf.may_contain(probes[i % 1000])
+        t_mc = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        for _ in range(200):
+            blob = bf.to_bytes()
+        t_tb = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        for _ in range(20):
+            cls.build_from_keys_and_fp_rate(keys, 0.001, **kw) if cls is BloomFilter else None
+        t_bk = time.perf_counter() - t0
+        out[name] = {"add_us_per_key_incl_flush": round(t_add / 1000 * 1e6, 2),
+                     "may_contain_us": round(t_mc / reps * 1e6, 2), "to_bytes_us": round(t_tb / 200 * 1e6, 2),
+                     "hits": hits, "bitmap_sha16": __import__("hashlib").sha256(blob).hexdigest()[:16]}
+        if cls is BloomFilter:
+            out[name]["build_from_keys_1k_us"] = round(t_bk / 20 * 1e6, 1)
+    out["identical"] = (out["pebbledb_amd"]["bitmap_sha16"] == out["reference_port"]["bitmap_sha16"]
+                        and out["pebbledb_amd"]["hits"] == out["reference_port"]["hits"])
+    return out
+
+
 def all_reduce_scalar(torch, dist, value, op, dtype):
     """max / min of a scalar over ranks (RCCL: a device tensor; gloo rehearsal: a host one)."""
     dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
@@ -832,6 +876,8 @@ def main():
             out["host_inclusive"] = host_inc
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(nb_bytes, k, kind, args.cpu_seconds)
+            if args.config == "c1":
+                out["dropin_latency"] = dropin_latency(local)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

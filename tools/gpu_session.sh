@@ -104,6 +104,8 @@ for step in "$@"; do
     chunks) for c in ${PBF_CHUNKS:-2000000 4000000 6000000 10000000}; do PBF_PROBE_CHUNK=$c run chunk_$c 300 python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-host-inclusive; done
             run chunk_none 300 python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-host-inclusive ;;
     pytest_new) run pytest_new 900 python -u -m pytest tests/test_gpu_multi.py tests/test_gpu_dropin.py tests/test_gpu_distributed.py tests/test_gpu_lsm_get.py -m gpu -x -v -rf --timeout 600 --timeout-method thread ;;
+    bench_c1) run bench_c1 300 python bench.py --config c1 --steps 50 --warmup 5 ;;
+    bench_sst2) run bench_sst 600 python bench.py --config sst --steps 20 --warmup 3 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
