@@ -143,6 +143,9 @@ int pbf_last_build_mode(pbf_filter_t* f);
 int pbf_set_probe_mode(pbf_filter_t* f, int mode);
 int pbf_last_probe_mode(pbf_filter_t* f);
 uint32_t pbf_last_probe_detail(pbf_filter_t* f);
+/* How the last tiled build ran: PBF_DETAIL_RING or _SORT | log2(tiles per super-tile) << 8 |
+ * (keys per sub-chunk / 256) << 12. */
+uint32_t pbf_last_build_detail(pbf_filter_t* f);
 
 /* Release the device's pooled working memory (waits for its last users); the next call
  * re-allocates what it needs.  pbf_scratch_bytes reports what the pool holds now. */

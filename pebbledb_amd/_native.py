@@ -53,6 +53,7 @@ SIGNATURES = {
     "pbf_set_probe_mode": (_int, [_vp, _int]),
     "pbf_last_probe_mode": (_int, [_vp]),
     "pbf_last_probe_detail": (_u32, [_vp]),
+    "pbf_last_build_detail": (_u32, [_vp]),
     "pbf_may_contain": (_int, [_vp, ctypes.c_char_p, _u64, ctypes.POINTER(_int)]),
     "pbf_trim": (_int, [_int]),
     "pbf_scratch_bytes": (_int, [_int, ctypes.POINTER(_u64)]),

@@ -320,6 +320,11 @@ class BloomFilter:
         return 0 if self._h is None else int(_native.lib().pbf_last_probe_detail(self._h))
 
     @property
+    def last_build_detail(self) -> int:
+        """PBF_DETAIL_RING/SORT | log2(tiles per super-tile) << 8 | (keys per sub-chunk / 256) << 12."""
+        return 0 if self._h is None else int(_native.lib().pbf_last_build_detail(self._h))
+
+    @property
     def last_build_mode(self) -> int:
         return 0 if self._h is None else _native.lib().pbf_last_build_mode(self._h)
 

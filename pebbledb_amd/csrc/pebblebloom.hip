@@ -292,6 +292,7 @@ struct pbf_filter {
     int probe_mode = PBF_PROBE_AUTO;
     int last_probe_mode = 0;
     uint32_t last_probe_detail = 0;  // PBF_DETAIL_* of the last probe
+    uint32_t last_build_detail = 0;  // PBF_DETAIL_* | sb << 8 | (kps / 256) << 12 of the last tiled build
     Scratch* sc = nullptr;           // leased for the current call
     uint64_t* dpop = nullptr;
     hipEvent_t ev = nullptr;       // stream joins of multi-filter probes
@@ -447,6 +448,29 @@ uint32_t ring_entries(uint32_t B, uint32_t k, bool probe, uint32_t tb) {
     return uint64_t(kRingKeysPerSub) * k * 4 <= uint64_t(B) * rc ? rc : 0;
 }
 
+// Ring BUILD geometry for any tile count: rings of 32 entries (64-B groups) per super-tile of
+// 2^sb tiles, with nsup = ceil(B / 2^sb) <= 1024 super-tiles (128 KiB of rings), and a sub-chunk
+// of kps keys small enough that a super-tile receives <= GS/2 = 8 positions per sub-chunk on
+// average.  C2 (B = 1024, k = 6): sb 0, kps 1024 (unchanged); C3 (B = 4096, k = 8): sb 2, kps
+// 1024; C4 (B = 1714, k = 10): sb 1, kps 512.  Returns false when no geometry fits.
+bool ring_build_geometry(uint32_t B, uint32_t k, uint32_t* sb, uint32_t* nsup, uint32_t* kps) {
+    const int ov = part_override();
+    if (ov == 1 || k > 16 || k == 0) return false;
+    uint32_t s = 0;
+    while (((B + (1u << s) - 1) >> s) > 1024) ++s;
+    if (s > 3) return false;
+    const uint32_t ns = (B + (1u << s) - 1) >> s;
+    for (uint32_t kp = 1024; kp >= 256; kp /= 2) {
+        if (uint64_t(kp) * k * 4 <= uint64_t(ns) * 32 || (ov == 2 && kp == 256)) {
+            *sb = s;
+            *nsup = ns;
+            *kps = kp;
+            return true;
+        }
+    }
+    return false;
+}
+
 // Gather LDS = the key bitmap of a partition workgroup + one u16 run-boundary row (`row`
 // entries) per tile of the split.  Splits start at gather_splits() and double (up to 64) while
 // the workgroup does not fit, so large batches stay in one pipeline.
@@ -459,9 +483,14 @@ void set_gather(PartPlan& pl, uint32_t B, uint32_t row, uint32_t nf = 1) {
     pl.lds_gather = lds(S);
 }
 
-PartPlan plan_ring(uint32_t B, uint32_t k, uint64_t n, uint32_t rc, double share, uint32_t nf = 1) {
+PartPlan plan_ring(uint32_t B, uint32_t k, uint64_t n, uint32_t rc, double share, uint32_t nf = 1,
+                   uint32_t sb = 0, uint32_t kps_ = kRingKeysPerSub) {
     PartPlan pl{};
-    const uint64_t kps = kRingKeysPerSub;
+    const uint64_t kps = kps_;
+    const uint32_t nsup = (B + (1u << sb) - 1) >> sb;
+    share = std::min(1.0, share * double(1u << sb));  // a super-tile holds 2^sb tiles
+    pl.pg.sb = sb;
+    pl.pg.nsup = nsup;
     const uint64_t G0 = std::min<uint64_t>(256, std::max<uint64_t>(1, (n + kps - 1) / kps));
     uint64_t kpw = (n + G0 - 1) / G0;
     kpw = ((kpw + kps - 1) / kps) * kps;
@@ -474,7 +503,7 @@ PartPlan plan_ring(uint32_t B, uint32_t k, uint64_t n, uint32_t rc, double share
     const double mu = double(kpw) * k * share;
     const uint64_t cap = uint64_t(mu + 8.0 * std::sqrt(mu) + 32.0);
     pl.pg.cap = uint32_t(((cap + 31) / 32) * 32);
-    pl.lds_part = size_t((2 * B + 16 * 128 + 3) & ~3u) * 4 + size_t(B) * rc * 4;
+    pl.lds_part = size_t((2 * nsup + 16 * 128 + 3) & ~3u) * 4 + size_t(nsup) * rc * 4;
     set_gather(pl, B, pl.pg.nq + 1, nf);
     return pl;
 }
@@ -496,6 +525,7 @@ PartPlan plan_partition(uint32_t B, uint32_t k, int km, uint64_t n, bool probe, 
     pl.pg.kps = uint32_t(kps);
     pl.pg.kpw = kpw;
     pl.pg.nsub = uint32_t(kpw / kps);
+    pl.pg.nsup = B;
     const double mu = double(kpw) * k * share;
     const uint64_t cap = uint64_t(mu + 8.0 * std::sqrt(mu) + 32.0);
     pl.pg.cap = uint32_t(((cap + 31) / 32) * 32);
@@ -528,7 +558,12 @@ double busiest_tile_share(const TileMap& tm) {
 PartPlan plan_for(const TileMap& tm, uint32_t k, int km, uint64_t n, bool probe, uint32_t nf = 1) {
     const uint32_t B = tm.nbuckets;
     const double share = busiest_tile_share(tm);
-    const uint32_t rc = ring_entries(B, k, probe, tm.tb);
+    uint32_t sb, nsup, kps;
+    if (!probe && ring_build_geometry(B, k, &sb, &nsup, &kps)) {
+        const PartPlan pl = plan_ring(B, k, n, 32, share, 1, sb, kps);
+        if (pl.pg.cap < (1u << 20)) return pl;
+    }
+    const uint32_t rc = probe ? ring_entries(B, k, probe, tm.tb) : 0;
     if (rc) {
         const PartPlan pl = plan_ring(B, k, n, rc, share, nf);
         if (pl.pg.cap < (1u << 20)) return pl;  // flush descriptors hold a region position in 20 bits
@@ -542,8 +577,8 @@ int run_tiled(pbf_filter_t* f, const Batch& b) {
     const uint32_t k = f->k;
     const PartPlan pl = plan_for(tm, k, b.km, b.n, false);
     const PartGeom& pg = pl.pg;
-    HIP_TRY(f->sc->regions.ensure(size_t(pg.G) * B * pg.cap * 4));
-    HIP_TRY(f->sc->fill.ensure(size_t(pg.G) * B * 4));
+    HIP_TRY(f->sc->regions.ensure(size_t(pg.G) * pg.nsup * pg.cap * 4));
+    HIP_TRY(f->sc->fill.ensure(size_t(pg.G) * pg.nsup * 4));
     HIP_TRY(f->sc->ovf.ensure(std::max<uint64_t>(b.n * k, 1) * 4));
     HIP_TRY(f->sc->ovf_count.ensure(64));
     if (!f->sc->ovf_init) {  // two counters, used alternately; each build's k_ovf_build zeroes the other
@@ -581,9 +616,16 @@ int run_tiled(pbf_filter_t* f, const Batch& b) {
     HIP_TRY(err);
     CHECK_LAUNCH();
     const size_t lds_tile = ((size_t(1) << tm.tb) / 32 + pg.G) * 4;
-    HIP_TRY(allow_lds(k_tile_build, lds_tile));
-    k_tile_build<<<B, 1024, lds_tile, s>>>(tm, pg, regions, fill, f->bitmap, f->pristine ? 1 : 0);
+    if (pg.ring && pg.sb > 0) {
+        HIP_TRY(allow_lds(k_tile_build<true>, lds_tile));
+        const uint32_t grid = ((pg.nsup + 7) / 8) * 8 * (1u << pg.sb);
+        k_tile_build<true><<<grid, 1024, lds_tile, s>>>(tm, pg, regions, fill, f->bitmap, f->pristine ? 1 : 0);
+    } else {
+        HIP_TRY(allow_lds(k_tile_build<false>, lds_tile));
+        k_tile_build<false><<<B, 1024, lds_tile, s>>>(tm, pg, regions, fill, f->bitmap, f->pristine ? 1 : 0);
+    }
     CHECK_LAUNCH();
+    f->last_build_detail = (pg.ring ? PBF_DETAIL_RING : PBF_DETAIL_SORT) | (pg.sb << 8) | ((pg.kps / 256) << 12);
     k_ovf_build<<<256, 256, 0, s>>>(tm, ovf, ovf_count, f->bitmap, ovf_next);
     CHECK_LAUNCH();
     f->pristine = false;
@@ -1525,6 +1567,7 @@ int pbf_set_probe_mode(pbf_filter_t* f, int mode) {
 
 int pbf_last_probe_mode(pbf_filter_t* f) { return f ? f->last_probe_mode : 0; }
 uint32_t pbf_last_probe_detail(pbf_filter_t* f) { return f ? f->last_probe_detail : 0; }
+uint32_t pbf_last_build_detail(pbf_filter_t* f) { return f ? f->last_build_detail : 0; }
 
 int pbf_encode_data_blocks(int device, const uint8_t* keys, const uint64_t* key_offsets, const uint8_t* values,
                            const uint64_t* value_offsets, uint64_t n, const uint64_t* block_first,

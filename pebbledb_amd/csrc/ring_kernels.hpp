@@ -59,7 +59,11 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
                                                     ProbeSet ps, int sbase, const uint32_t* __restrict__ alive,
                                                     uint32_t* __restrict__ hw_init) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-    const uint32_t B = tm.nbuckets;
+    // rings per super-tile of 2^sb tiles (builds of filters with more tiles than the LDS has
+    // rings for; probes: sb = 0, nsup = the tile count)
+    const uint32_t B = pg.nsup;
+    const uint32_t shift = tm.tb + pg.sb;
+    const uint32_t kps = pg.kps;  // keys per sub-chunk (<= 1024 threads)
     const uint32_t RC = pg.ring, GS = RC / 2, rmask = RC - 1;
     const uint32_t tid = threadIdx.x, nt = blockDim.x;
     const uint32_t lane = tid & 63, wave = tid >> 6;
@@ -96,14 +100,14 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
     auto load_batch = [&](uint64_t c0) {
 #pragma unroll
         for (int u = 0; u < P; ++u) {
-            const uint64_t i = c0 + uint64_t(u) * kRingKeysPerSub + tid;
+            const uint64_t i = c0 + uint64_t(u) * kps + tid;
             aw[u] = (alive && i < k1) ? alive[i >> 5] : ~0u;
             if constexpr (F16) kw[u] = ld_stream_nt<PBF_NT_KEYS != 0>(reinterpret_cast<const uint32_t*>(ks.data) + min(i, n - 1) * 4);
         }
     };
     load_batch(k0);
     uint32_t j = 0;
-    for (uint64_t c0 = k0; c0 < k1; c0 += uint64_t(P) * kRingKeysPerSub) {
+    for (uint64_t c0 = k0; c0 < k1; c0 += uint64_t(P) * kps) {
         uint4 cw[F16 ? P : 1];
         uint32_t ca[P];
 #pragma unroll
@@ -111,14 +115,14 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
             if constexpr (F16) cw[u] = kw[u];
             ca[u] = aw[u];
         }
-        if (c0 + uint64_t(P) * kRingKeysPerSub < k1) load_batch(c0 + uint64_t(P) * kRingKeysPerSub);
+        if (c0 + uint64_t(P) * kps < k1) load_batch(c0 + uint64_t(P) * kps);
 #pragma unroll
         for (int u = 0; u < P; ++u, ++j) {
-            const uint64_t s0 = c0 + uint64_t(u) * kRingKeysPerSub;
+            const uint64_t s0 = c0 + uint64_t(u) * kps;
             if (s0 >= k1) break;
             const uint64_t i = s0 + tid;
             // a probe round after the first hashes only keys that are still possible members
-            const bool live = i < k1 && ((ca[u] >> (i & 31)) & 1u);
+            const bool live = tid < kps && i < k1 && ((ca[u] >> (i & 31)) & 1u);
             uint32_t pos[KMAX], slot[KMAX], hd[KMAX];
             auto hash = [&] {
                 auto emit = [&](int s, uint32_t h) { pos[s] = ring_pos<POW2>(h, tm); };
@@ -142,7 +146,7 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
 #pragma unroll
                 for (int s = 0; s < KMAX; ++s) {
                     if (s < k) {
-                        const unsigned long long v = atomicAdd(ht + (pos[s] >> tm.tb), 1ull);
+                        const unsigned long long v = atomicAdd(ht + (pos[s] >> shift), 1ull);
                         slot[s] = uint32_t(v);
                         hd[s] = uint32_t(v >> 32);
                     }
@@ -152,7 +156,7 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
 #pragma unroll
                 for (int s = 0; s < KMAX; ++s) {
                     if (s < k) {
-                        const uint32_t p = pos[s], b = p >> tm.tb, e = slot[s];
+                        const uint32_t p = pos[s], b = p >> shift, e = slot[s];
                         if (e - hd[s] < RC && e < cap)
                             ring[b * RC + (e & rmask)] =
                                 PROBE ? (((j & 3u) << 30) | (tid << kSlotShift) | (p & lmask)) : p;

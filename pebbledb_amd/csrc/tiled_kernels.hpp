@@ -128,6 +128,8 @@ struct PartGeom {
     uint64_t kpw;      // keys per workgroup (= nsub * kps)
     uint32_t nq;       // ring partition: pref groups (4 sub-chunks each) per workgroup
     uint32_t ring;     // ring partition: LDS ring entries per tile (0 = counting-sort partition)
+    uint32_t sb;       // ring build: log2 tiles per super-tile (regions are per super-tile)
+    uint32_t nsup;     // ring partition: super-tiles (= tiles when sb = 0)
 };
 
 constexpr uint32_t kSlotShift = 20;   // probe entry = slot-in-sub-chunk << 20 | position in tile
@@ -398,30 +400,44 @@ __device__ __forceinline__ void store_tile(const uint32_t* tile, uint32_t* __res
     }
 }
 
-__device__ __forceinline__ void or_bits4(uint32_t* tile, uint4 v, uint32_t e, uint32_t f, uint32_t lmask) {
-    uint32_t p = v.x & lmask;
-    if (e < f) atomicOr(tile + (p >> 5), 1u << (p & 31));
-    p = v.y & lmask;
-    if (e + 1 < f) atomicOr(tile + (p >> 5), 1u << (p & 31));
-    p = v.z & lmask;
-    if (e + 2 < f) atomicOr(tile + (p >> 5), 1u << (p & 31));
-    p = v.w & lmask;
-    if (e + 3 < f) atomicOr(tile + (p >> 5), 1u << (p & 31));
+// OR the in-fill entries of a 4-entry piece into the LDS tile.  SUPER: the region holds a whole
+// super-tile's positions; only those of this workgroup's tile t (p >> tb == t) are taken.
+template <bool SUPER = false>
+__device__ __forceinline__ void or_bits4(uint32_t* tile, uint4 v, uint32_t e, uint32_t f, uint32_t lmask,
+                                         uint32_t tb = 0, uint32_t t = 0) {
+    const uint32_t vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t p = vv[q] & lmask;
+        if (e + q < f && (!SUPER || (vv[q] >> tb) == t)) atomicOr(tile + (p >> 5), 1u << (p & 31));
+    }
 }
 
 // ------------------------------------------------------------------ build: tiles
 // One workgroup per tile.  A wave (64 lanes x 16-byte loads = 256 entries) covers one region
 // per step and keeps U regions of loads in flight.
+// SUPER (ring build with 2^sb tiles per super-tile): workgroup (super-tile s, part h) builds
+// tile t = s * 2^sb + h from the regions of s.  The 2^sb workgroups of one super-tile are dealt
+// onto one XCD and dispatched together (block x = ((s / 8) * 2^sb + h) * 8 + s % 8; round-robin
+// XCD placement, speed only), so they stream the same region entries and all but the first
+// read them from that XCD's L2.
+template <bool SUPER>
 __global__ void __launch_bounds__(1024) k_tile_build(TileMap tm, PartGeom pg, const uint32_t* __restrict__ regions,
                                                      const uint32_t* __restrict__ fill, uint32_t* __restrict__ bitmap,
                                                      int pristine) {
     extern __shared__ uint32_t smem[];
-    const uint32_t B = tm.nbuckets, G = pg.G, cap = pg.cap;
-    const uint32_t b = blockIdx.x;
+    const uint32_t B = pg.nsup, G = pg.G, cap = pg.cap;
+    uint32_t b = blockIdx.x, t = blockIdx.x;  // region column (super-tile) and the tile built
+    if constexpr (SUPER) {
+        const uint32_t x = blockIdx.x, parts = 1u << pg.sb, q = x >> 3;
+        b = (q >> pg.sb) * 8 + (x & 7);
+        t = (b << pg.sb) + (q & (parts - 1));
+        if (b >= pg.nsup || t >= tm.nbuckets) return;
+    }
     const uint32_t W = 1u << (tm.tb - 5);
     uint32_t* tile = smem;       // W
     uint32_t* fills = tile + W;  // G
-    const uint64_t w0 = tile_word0(b, tm);
+    const uint64_t w0 = tile_word0(t, tm);
     const uint32_t nw = uint32_t(min<uint64_t>(W, tm.total_words - w0));
     const uint32_t tid = threadIdx.x, nt = blockDim.x;
     for (uint32_t q = tid; q < G; q += nt) fills[q] = fill[uint64_t(b) * G + q];
@@ -450,15 +466,15 @@ __global__ void __launch_bounds__(1024) k_tile_build(TileMap tm, PartGeom pg, co
         }
 #pragma unroll
         for (int u = 0; u < U; ++u)
-            if (lane * 4 < f[u]) or_bits4(tile, v[u], lane * 4, f[u], lmask);
+            if (lane * 4 < f[u]) or_bits4<SUPER>(tile, v[u], lane * 4, f[u], lmask, tm.tb, t);
     }
     // regions holding more than 256 entries
     if (cap > 256) {
         for (uint32_t q = wave; q < G; q += nwaves) {
             const uint32_t fq = fills[q];
             for (uint32_t c = 64 + lane; c * 4 < fq; c += 64)
-                or_bits4(tile, ld_stream(regions + region_id(q, b, G, B) * cap + c * 4), c * 4, fq,
-                         lmask);
+                or_bits4<SUPER>(tile, ld_stream(regions + region_id(q, b, G, B) * cap + c * 4), c * 4, fq,
+                                lmask, tm.tb, t);
         }
     }
     lds_barrier();
