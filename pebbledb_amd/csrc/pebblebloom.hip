@@ -12,6 +12,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <thread>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -296,7 +297,6 @@ struct pbf_filter {
     Scratch* sc = nullptr;           // leased for the current call
     uint64_t* dpop = nullptr;
     hipEvent_t ev = nullptr;       // stream joins of multi-filter probes
-    hipEvent_t done_ev = nullptr;  // blocking waits (pbf_sync)
     std::mutex mu;                 // one host thread inside the handle at a time
 };
 
@@ -417,6 +417,7 @@ struct PartPlan {
     size_t lds_part;
     size_t lds_gather;  // probes: per gather workgroup
     uint32_t gsplit;    // probes: gather splits over tile ranges (grid G x gsplit)
+    uint32_t gtq;       // ring gather: quad-table bytes per tile (0 = binary search)
 };
 
 // Partition strategy: PBF_PART=sort|ring forces one (tests, measurements); default auto.
@@ -481,6 +482,21 @@ void set_gather(PartPlan& pl, uint32_t B, uint32_t row, uint32_t nf = 1) {
     while (lds(S) > 156 * 1024 && S < 64 && S < B) S *= 2;
     pl.gsplit = S;
     pl.lds_gather = lds(S);
+    pl.gtq = 0;
+    // the ring gather's quad table, when groups fit a byte and the workgroup stays small enough
+    // for 4 per CU (PBF_GATHER_QTAB=0 turns it off)
+    static const bool qtab_on = [] {
+        const char* e = std::getenv("PBF_GATHER_QTAB");
+        return !(e && std::atoi(e) == 0);
+    }();
+    if (qtab_on && pl.pg.ring && row <= 255) {
+        const uint32_t tq = pl.pg.cap / 4;
+        const size_t with = ((pl.lds_gather + 3) & ~size_t(3)) + size_t((B + S - 1) / S) * tq + 4;
+        if (with <= 38 * 1024) {
+            pl.gtq = tq;
+            pl.lds_gather = with;
+        }
+    }
 }
 
 PartPlan plan_ring(uint32_t B, uint32_t k, uint64_t n, uint32_t rc, double share, uint32_t nf = 1,
@@ -723,7 +739,7 @@ int run_tiled_probe_set(pbf_filter_t* f, pbf_filter_t* const* fs, uint32_t nf, c
             }
             CHECK_LAUNCH();
             gring<<<grid, 512, pl.lds_gather, s>>>(tm, pg, b.n, regions, R, fill, subcnt, neg, alive, outs[0] + hm_off,
-                                                  hw, nf, r_words, neg_words);
+                                                  hw, nf, r_words, neg_words, pl.gtq);
             CHECK_LAUNCH();
             if (use_hw) {
                 for (uint32_t i = 0; i < nf; ++i) {
@@ -1047,25 +1063,25 @@ int check_keys(pbf_filter_t* f, const uint8_t* keys, const uint64_t* offsets, ui
 }
 
 // Wait for everything queued on f's stream.  Polls first (a caller that waits is about to use
-// the results, and a blocking wake-up costs tens of microseconds), then blocks on an event
-// created with hipEventBlockingSync, so a long wait does not keep a host core spinning
-// (PBF_SPIN_US sets the polling budget, default 200 us).
+// the results), then keeps polling with sleeps that back off from 10 us to 200 us, so a long
+// wait costs a host core almost nothing and does not depend on an interrupt-driven wake-up
+// (PBF_SPIN_US sets the pure polling budget, default 200 us).
 int wait_stream(pbf_filter_t* f) {
     static const long spin_us = [] {
         const char* e = std::getenv("PBF_SPIN_US");
         return e ? std::atol(e) : 200L;
     }();
     const auto t0 = std::chrono::steady_clock::now();
+    long nap_us = 10;
     for (;;) {
         const hipError_t e = hipStreamQuery(f->stream);
         if (e == hipSuccess) return PBF_OK;
         if (e != hipErrorNotReady) return fail(PBF_ERR_HIP, std::string("hipStreamQuery: ") + hipGetErrorString(e));
-        if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(spin_us)) break;
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(spin_us)) {
+            std::this_thread::sleep_for(std::chrono::microseconds(nap_us));
+            nap_us = std::min(nap_us * 2, 200L);
+        }
     }
-    if (!f->done_ev) HIP_TRY(hipEventCreateWithFlags(&f->done_ev, hipEventBlockingSync | hipEventDisableTiming));
-    HIP_TRY(hipEventRecord(f->done_ev, f->stream));
-    HIP_TRY(hipEventSynchronize(f->done_ev));
-    return PBF_OK;
 }
 
 #define WAIT(f)                       \
@@ -1315,7 +1331,6 @@ int pbf_destroy(pbf_filter_t* f) {
     if (f->bitmap) (void)hipFree(f->bitmap);
     if (f->dpop) (void)hipFree(f->dpop);
     if (f->ev) (void)hipEventDestroy(f->ev);
-    if (f->done_ev) (void)hipEventDestroy(f->done_ev);
     if (f->stream) (void)hipStreamDestroy(f->stream);
     delete f;
     return PBF_OK;

@@ -269,7 +269,9 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
 // S = 1 and nf = 1 writes the hit-mask words directly; otherwise the words are ANDed into
 // hw + f * neg_stride (one u32 per 32 keys, preset to all ones) and k_hw_to_hitmask writes
 // each filter's hit mask.
-//   LDS: nf x kbits[kpw/32], pref rows of the split's tiles as u16 ((B/S) x (nq+1)).
+//   LDS: nf x kbits[kpw/32], pref rows of the split's tiles as u16 ((B/S) x (nq+1)), and with
+//   `qtab` (tq = cap/4 bytes per tile, nq < 255) the group of every 4-entry quad's first entry,
+//   so a failed quad starts from its group instead of a binary search over the row.
 // NFM: compile-time bound on nf (1 for a single filter: no per-filter registers or loops).
 template <int NFM>
 __global__ void __launch_bounds__(512) k_gather_ring(TileMap tm, PartGeom pg, uint64_t n,
@@ -278,7 +280,7 @@ __global__ void __launch_bounds__(512) k_gather_ring(TileMap tm, PartGeom pg, ui
                                                      const uint32_t* __restrict__ pref,
                                                      const uint32_t* __restrict__ neg, const uint32_t* __restrict__ alive,
                                                      uint8_t* __restrict__ hitmask, uint32_t* __restrict__ hw,
-                                                     uint32_t nf, uint64_t r_stride, uint64_t neg_stride) {
+                                                     uint32_t nf, uint64_t r_stride, uint64_t neg_stride, uint32_t tq) {
     extern __shared__ uint32_t smem[];
     if constexpr (NFM == 1) nf = 1;
     const uint32_t B = tm.nbuckets, cap = pg.cap, wpr = cap / 32, nqs = pg.nq + 1;
@@ -294,10 +296,23 @@ __global__ void __launch_bounds__(512) k_gather_ring(TileMap tm, PartGeom pg, ui
     const uint32_t kw = uint32_t((pg.kpw + 31) / 32);
     uint32_t* kbits = smem;                                         // nf x kw words
     uint16_t* lpref = reinterpret_cast<uint16_t*>(kbits + nf * kw);  // nb * nqs (values <= cap < 2^16)
+    uint8_t* qtab = reinterpret_cast<uint8_t*>(lpref + ((nb * nqs + 1) & ~1u));  // nb * tq (tq > 0)
     const uint32_t* gp = pref + uint64_t(g) * nqs * B;  // [q][b] in memory, [b][q] in LDS
     for (uint32_t x = tid; x < nb * nqs; x += nt) {
         const uint32_t q = x / nb, bb = x - q * nb;
         lpref[bb * nqs + q] = uint16_t(gp[uint64_t(q) * B + b_lo + bb]);
+    }
+    if (tq) {
+        lds_barrier();
+        // quad c of tile bb starts in group q when pref[q] <= 4c < pref[q+1]: each (tile, group)
+        // writes the quads whose first entry it holds (pref[nq] = the fill, the last group open)
+        for (uint32_t x = tid; x < nb * nqs; x += nt) {
+            const uint32_t bb = x / nqs, q = x - bb * nqs;
+            const uint16_t* pb = lpref + bb * nqs;
+            const uint32_t lo = (uint32_t(pb[q]) + 3) >> 2;
+            const uint32_t hi = q + 1 < nqs ? (uint32_t(pb[q + 1]) + 3) >> 2 : tq;
+            for (uint32_t c = lo; c < min(hi, tq); ++c) qtab[bb * tq + c] = uint8_t(q);
+        }
     }
     for (uint32_t f = 0; f < nf; ++f) {
         for (uint32_t w = tid; w < kw; w += nt) {
@@ -346,14 +361,19 @@ __global__ void __launch_bounds__(512) k_gather_ring(TileMap tm, PartGeom pg, ui
                         any |= fl[f];
                     }
                     if (any) {
-                        // q = the last group with pref[q] <= r (pref non-decreasing, pref[0] = 0);
-                        // a fixed-trip binary search keeps the wave's lanes together
+                        // q = the last group with pref[q] <= r (pref non-decreasing, pref[0] = 0):
+                        // from the quad table, else a fixed-trip binary search
                         const uint16_t* pb = lpref + (b - b_lo) * nqs;
-                        uint32_t lo = 0, len = nqs;
-                        while (len > 1) {
-                            const uint32_t half = len >> 1;
-                            if (pb[lo + half] <= r) lo += half;
-                            len -= half;
+                        uint32_t lo = 0;
+                        if (tq) {
+                            lo = qtab[(b - b_lo) * tq + (r >> 2)];
+                        } else {
+                            uint32_t len = nqs;
+                            while (len > 1) {
+                                const uint32_t half = len >> 1;
+                                if (pb[lo + half] <= r) lo += half;
+                                len -= half;
+                            }
                         }
                         const uint32_t vv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
 #pragma unroll

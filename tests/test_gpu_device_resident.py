@@ -110,7 +110,7 @@ def test_config2_full_size_properties(oracle):
     assert np.array_equal(h[n // 8: n // 8 + 125000], oracle.probe(want, k, qs, omp=True))
 
 
-@pytest.mark.timeout(300)
+@pytest.mark.timeout(150)
 def test_config4_full_size_product_sizing(oracle):
     """C4: one of the eight 125M-key SSTable filters with pebbledb's product sizing
     (sstable.py:274, fp 0.001 → nb_bytes 224,649,806, k = 10: non-power-of-two m, the
@@ -136,7 +136,7 @@ def test_config4_full_size_product_sizing(oracle):
     assert got == want.tobytes()
 
 
-@pytest.mark.timeout(300)
+@pytest.mark.timeout(150)
 def test_config3_full_size_varlen_large_m(oracle):
     """C3: 100M variable-length keys (8..64 B) into m = 2^33 bits (nb_bytes = 2^30), k = 8 — the
     m > 2^32 index map where only [0, 2^31) and [m - 2^31, m) are reachable.  Tiled build ==

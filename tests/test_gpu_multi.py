@@ -178,7 +178,7 @@ def _c5_probe_and_check(oracle, fs, want, q, nq, k=6, sample=(0, 1_000_000)):
     return got, detail
 
 
-@pytest.mark.timeout(600)
+@pytest.mark.timeout(150)
 def test_c5_full_geometry_fused_ring_gather(oracle):
     """BASELINE.json configs[4] on one GPU as bench.py runs it: 8 filters (nb_bytes = 2^27,
     k = 6, 10M keys each) and one device multi-probe of 20M + 37 keys (half members spread over
@@ -207,7 +207,7 @@ def test_c5_full_geometry_fused_ring_gather(oracle):
         assert fp <= 3 * (nq - half) * fill ** 6 + 20, (f, fp)
 
 
-@pytest.mark.timeout(600)
+@pytest.mark.timeout(150)
 @pytest.mark.parametrize("nf", [2, 5])
 def test_c5_geometry_small_sets_ragged_and_spills(oracle, nf):
     """The same ring + fused path with 2 and 5 filters, a ragged batch, and keys repeated 60k and
