@@ -308,6 +308,14 @@ int enter(pbf_filter_t* f) {
     return PBF_OK;
 }
 
+// hipEventQuery / hipStreamQuery report "not ready" as an error code, and HIP keeps it as the
+// thread's last error; the launch checks (hipGetLastError) must not see it.
+bool event_done(hipEvent_t e) {
+    const hipError_t r = hipEventQuery(e);
+    if (r != hipSuccess) (void)hipGetLastError();
+    return r == hipSuccess;
+}
+
 // Lease a scratch set of f's device for work enqueued on f's stream (RAII).  Prefers a set
 // whose previous work is done or was on this same stream; creates one while fewer than
 // max_scratch_sets() exist; otherwise takes a free set and orders this stream after its
@@ -324,7 +332,7 @@ class Lease {
             for (Scratch* s : pool.sets) {
                 if (s->leased) continue;
                 if (!any) any = s;
-                if (!s->last || s->last_stream == f_->stream || hipEventQuery(s->last) == hipSuccess) {
+                if (!s->last || s->last_stream == f_->stream || event_done(s->last)) {
                     pick = s;
                     break;
                 }
@@ -1076,6 +1084,7 @@ int wait_stream(pbf_filter_t* f) {
     for (;;) {
         const hipError_t e = hipStreamQuery(f->stream);
         if (e == hipSuccess) return PBF_OK;
+        (void)hipGetLastError();  // "not ready" is not an error (see event_done)
         if (e != hipErrorNotReady) return fail(PBF_ERR_HIP, std::string("hipStreamQuery: ") + hipGetErrorString(e));
         if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(spin_us)) {
             std::this_thread::sleep_for(std::chrono::microseconds(nap_us));
