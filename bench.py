@@ -789,7 +789,9 @@ def main():
     fp = int(np.unpackbits(hm, bitorder="little")[n:2 * n].sum())
     # a corrupted bitmap (e.g. all ones) still lets every member hit: the absent half must show
     # false positives at the filter's own rate, fill^k (fill measured on the device)
-    fill = bf.popcount() / m_bits
+    # positions a signed 32-bit hash can reach: all m, or 2^32 of them when m > 2^32
+    # (bloom_filter.py:47 floor-mod)
+    fill = bf.popcount() / min(m_bits, 2 ** 32)
     fp_expect = n * fill ** k
     fp_ok = fp <= 3 * fp_expect + 20
     if world > 1:

@@ -462,7 +462,8 @@ __global__ void __launch_bounds__(1024) k_tile_build(TileMap tm, PartGeom pg, co
             f[u] = q < G ? fills[q] : 0u;
             // unconditional loads, clamped to the filled part (idle lanes re-read its last line)
             const uint32_t lc = min(lane, (max(f[u], 1u) - 1) >> 2);
-            v[u] = ld_stream(regions + region_id(min(q, G - 1), b, G, B) * cap + lc * 4);
+            // siblings of a super-tile read these lines too: keep them in L2 (temporal loads)
+            v[u] = ld_stream_nt<!SUPER && PBF_NT_LOAD != 0>(regions + region_id(min(q, G - 1), b, G, B) * cap + lc * 4);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u)
@@ -473,8 +474,8 @@ __global__ void __launch_bounds__(1024) k_tile_build(TileMap tm, PartGeom pg, co
         for (uint32_t q = wave; q < G; q += nwaves) {
             const uint32_t fq = fills[q];
             for (uint32_t c = 64 + lane; c * 4 < fq; c += 64)
-                or_bits4<SUPER>(tile, ld_stream(regions + region_id(q, b, G, B) * cap + c * 4), c * 4, fq,
-                                lmask, tm.tb, t);
+                or_bits4<SUPER>(tile, ld_stream_nt<!SUPER && PBF_NT_LOAD != 0>(regions + region_id(q, b, G, B) * cap + c * 4),
+                                c * 4, fq, lmask, tm.tb, t);
         }
     }
     lds_barrier();
@@ -510,6 +511,7 @@ __device__ __forceinline__ uint32_t r_quad(uint32_t rw, uint32_t r) {
 // region).  Each lane tests its 4 entries in the LDS tile; four ballots give every word's 32
 // result bits, stored by the word's first lane.  `expand` = the LDS budget allows a per-word
 // region id table (else a binary search over the word prefix).
+template <bool NT>
 __device__ __forceinline__ void tile_probe_body(uint32_t* smem, uint32_t b, const TileMap& tm, const PartGeom& pg,
                                                 const uint32_t* __restrict__ regions, const uint32_t* __restrict__ fill,
                                                 const uint32_t* __restrict__ bitmap, uint32_t* __restrict__ R,
@@ -548,7 +550,7 @@ __device__ __forceinline__ void tile_probe_body(uint32_t* smem, uint32_t b, cons
             const uint32_t c = min(c0 + u * stride + wsub, total - 1);  // unconditional loads
             qq[u] = expand ? uint32_t(wq[c]) : bucket_of(wpre, G, c);
             word[u] = c - wpre[qq[u]];
-            v[u] = ld_stream(regions + region_id(qq[u], b, G, B) * cap + word[u] * 32 + l * 4);
+            v[u] = ld_stream_nt<NT>(regions + region_id(qq[u], b, G, B) * cap + word[u] * 32 + l * 4);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -579,7 +581,7 @@ __global__ void __launch_bounds__(1024) k_tile_probe(TileMap tm, PartGeom pg, co
                                                      const uint32_t* __restrict__ bitmap, uint32_t* __restrict__ R,
                                                      int expand) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-    tile_probe_body(smem, blockIdx.x, tm, pg, regions, fill, bitmap, R, expand);
+    tile_probe_body<PBF_NT_LOAD != 0>(smem, blockIdx.x, tm, pg, regions, fill, bitmap, R, expand);
 }
 
 // The tile test of a multi-filter probe in ONE launch: workgroup (tile b, filter f) for every
@@ -596,7 +598,8 @@ __global__ void __launch_bounds__(1024) k_tile_probe_set(TileMap tm, PartGeom pg
     const uint32_t f = t % nf;
     const uint32_t b = (t / nf) * 8 + (x & 7);
     if (b >= tm.nbuckets) return;
-    tile_probe_body(smem, b, tm, pg, regions, fill, ps.bm[f], R + f * r_stride, expand);
+    // the set's other workgroups of tile b read the same lines: temporal loads keep them in L2
+    tile_probe_body<false>(smem, b, tm, pg, regions, fill, ps.bm[f], R + f * r_stride, expand);
 }
 
 // Workgroup g owns keys [g*kpw, (g+1)*kpw) and regions (g, 0..B-1).  It reads each region once,
