@@ -462,12 +462,26 @@ uint32_t ring_entries(uint32_t B, uint32_t k, bool probe, uint32_t tb) {
 // of kps keys small enough that a super-tile receives <= GS/2 = 8 positions per sub-chunk on
 // average.  C2 (B = 1024, k = 6): sb 0, kps 1024 (unchanged); C3 (B = 4096, k = 8): sb 2, kps
 // 1024; C4 (B = 1714, k = 10): sb 1, kps 512.  Returns false when no geometry fits.
+//
+// Measured (profiles/r02/s2): super-tiles lose.  C3 (sb 2): ring partition 4.05 ms vs the
+// counting-sort partition's 5.11, but the 4 sibling tile builders do not find each other's
+// region lines in L2 and read them 4x (2.20 ms vs 0.80); C4 (sb 1, kps 512): both kernels slower
+// (5.03 + 5.44 vs 3.80 + 4.14 ms per 107M-key pipeline).  So sb > 0 is opt-in (PBF_RING_SUPER=1)
+// and only sb = 0 geometries (<= 1024 tiles) take the ring build by default.
+bool ring_super_on() {
+    static const bool v = [] {
+        const char* e = std::getenv("PBF_RING_SUPER");
+        return e && std::atoi(e) != 0;
+    }();
+    return v;
+}
+
 bool ring_build_geometry(uint32_t B, uint32_t k, uint32_t* sb, uint32_t* nsup, uint32_t* kps) {
     const int ov = part_override();
     if (ov == 1 || k > 16 || k == 0) return false;
     uint32_t s = 0;
     while (((B + (1u << s) - 1) >> s) > 1024) ++s;
-    if (s > 3) return false;
+    if (s > 3 || (s > 0 && !ring_super_on())) return false;
     const uint32_t ns = (B + (1u << s) - 1) >> s;
     for (uint32_t kp = 1024; kp >= 256; kp /= 2) {
         if (uint64_t(kp) * k * 4 <= uint64_t(ns) * 32 || (ov == 2 && kp == 256)) {

@@ -391,6 +391,28 @@ def test_tiled_partition_strategies_and_region_overflow(part, rounds):
     assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
 
 
+_SUPER_CHILD = """
+import sys; sys.path.insert(0, '.')
+import json
+from pebbledb_amd import BloomFilter, PackedKeys, _native
+from pebbledb_amd.keys import splitmix_hex_keys
+from oracle.oracle import COracle
+o = COracle()
+nb, k, n, sb, kps = json.loads(sys.argv[1])
+pk = PackedKeys.fixed(splitmix_hex_keys(31, 0, n))
+bf = BloomFilter(nb, k); bf.set_build_mode(2); bf.add_many(pk)
+d = bf.last_build_detail
+assert d & _native.PBF_DETAIL_RING and (d >> 8) & 0xF == sb and (d >> 12) * 256 == kps, hex(d)
+want = o.build(nb, k, pk, omp=True)
+assert bf.bitmap() == want.tobytes()
+more = PackedKeys.fixed(splitmix_hex_keys(32, 0, n // 3))
+bf.add_many(more)
+o.build(nb, k, more, bitmap=want, omp=True)
+assert bf.bitmap() == want.tobytes()
+print("ok")
+"""
+
+
 @pytest.mark.parametrize("nb,k,n,sb,kps", [
     (2 ** 28, 6, 3_000_000, 1, 1024),        # 2048 tiles: two per super-tile
     (2 ** 29, 8, 3_000_000, 2, 1024),        # 4096 tiles (C3's tile count): four per super-tile
@@ -398,20 +420,19 @@ def test_tiled_partition_strategies_and_region_overflow(part, rounds):
     (2 ** 30, 8, 2_000_000, 2, 1024),        # C3's m = 2^33 (only 2^32 positions reachable)
     (3 * 2 ** 26 + 5, 16, 1_000_000, 1, 256),  # odd nb_bytes, k = 16: small sub-chunks
 ])
-def test_ring_build_super_tiles(oracle, nb, k, n, sb, kps):
+def test_ring_build_super_tiles(nb, k, n, sb, kps):
     """The ring partition for filters with more tiles than LDS rings (SURVEY.md §8 a-4 at C3/C4
-    geometry): positions go to super-tiles of 2^sb tiles, 2^sb XCD-co-located tile builders
-    share each super-tile's regions.  Bit-exact vs the OpenMP oracle, onto a pristine and onto a
-    non-pristine bitmap, with the geometry checked via last_build_detail."""
-    pk = PackedKeys.fixed(splitmix_hex_keys(31, 0, n))
-    bf = BloomFilter(nb, k)
-    bf.set_build_mode(PBF_BUILD_TILED)
-    bf.add_many(pk)
-    d = bf.last_build_detail
-    assert d & _native.PBF_DETAIL_RING and (d >> 8) & 0xF == sb and (d >> 12) * 256 == kps, hex(d)
-    want = oracle.build(nb, k, pk, omp=True)
-    assert bf.bitmap() == want.tobytes()
-    more = PackedKeys.fixed(splitmix_hex_keys(32, 0, n // 3))
-    bf.add_many(more)
-    oracle.build(nb, k, more, bitmap=want, omp=True)
-    assert bf.bitmap() == want.tobytes()
+    geometry; opt-in, PBF_RING_SUPER=1, measured slower than the counting-sort partition):
+    positions go to super-tiles of 2^sb tiles, 2^sb XCD-co-located tile builders share each
+    super-tile's regions.  Bit-exact vs the OpenMP oracle, onto a pristine and onto a
+    non-pristine bitmap, with the geometry checked via last_build_detail (child process: the
+    switch is read once per process)."""
+    import json
+    import os
+    import subprocess
+    import sys
+    env = dict(os.environ, PBF_RING_SUPER="1")
+    r = subprocess.run([sys.executable, "-c", _SUPER_CHILD, json.dumps([nb, k, n, sb, kps])], env=env,
+                       capture_output=True, text=True, timeout=140,
+                       cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]

@@ -106,6 +106,12 @@ for step in "$@"; do
     pytest_new) run pytest_new 900 python -u -m pytest tests/test_gpu_multi.py tests/test_gpu_dropin.py tests/test_gpu_distributed.py tests/test_gpu_lsm_get.py -m gpu -x -v -rf --timeout 600 --timeout-method thread ;;
     bench_c1) run bench_c1 300 python bench.py --config c1 --steps 50 --warmup 5 ;;
     bench_sst2) run bench_sst 600 python bench.py --config sst --steps 20 --warmup 3 ;;
+    prof_c34ab) for part in ring sort; do
+                  PBF_PART=$part run prof_c3_$part 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_c3_$part -o run -- python bench.py --config c3 --steps 3 --warmup 1 --no-cpu-baseline --no-host-inclusive
+                  python tools/prof_summary.py gpurun_out/prof_c3_$part > gpurun_out/prof_c3_${part}_summary.txt 2>&1
+                  PBF_PART=$part run prof_c4_$part 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_c4_$part -o run -- python bench.py --config c4 --steps 2 --warmup 1 --no-cpu-baseline
+                  python tools/prof_summary.py gpurun_out/prof_c4_$part > gpurun_out/prof_c4_${part}_summary.txt 2>&1
+                done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
