@@ -1566,8 +1566,21 @@ int pbf_may_contain(pbf_filter_t* f, const uint8_t* key, uint64_t len, int* out)
             <<<1, 64, 0, f->stream>>>(ks, 1, int(f->k), f->im, f->bitmap, st->dev, int(f->k));
     });
     CHECK_LAUNCH();
-    WAIT(f);
-    const uint8_t hit = *reinterpret_cast<volatile uint8_t*>(st->host);
+    // The kernel's hit byte lands in mapped host memory as soon as it is stored (the key bytes
+    // were read before it), which is earlier than the stream's completion signal: poll the byte,
+    // and fall back to the stream wait (which also reports a failed kernel) after 2 ms.
+    volatile uint8_t* res = reinterpret_cast<volatile uint8_t*>(st->host);
+    const auto t0 = std::chrono::steady_clock::now();
+    uint8_t hit = 0xEE;
+    for (uint32_t spin = 0;; ++spin) {
+        hit = *res;
+        if (hit != 0xEE) break;
+        if ((spin & 255) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) {
+            WAIT(f);
+            hit = *res;
+            break;
+        }
+    }
     if (hit > 1) return fail(PBF_ERR_HIP, "one-key probe: result byte not written");
     *out = hit;
     f->last_probe_mode = PBF_PROBE_DIRECT;

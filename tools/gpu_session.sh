@@ -112,6 +112,7 @@ for step in "$@"; do
                   PBF_PART=$part run prof_c4_$part 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_c4_$part -o run -- python bench.py --config c4 --steps 2 --warmup 1 --no-cpu-baseline
                   python tools/prof_summary.py gpurun_out/prof_c4_$part > gpurun_out/prof_c4_${part}_summary.txt 2>&1
                 done ;;
+    gsweep) for sp in 4 8 16; do for qt in 0 1; do PBF_GATHER_SPLIT=$sp PBF_GATHER_QTAB=$qt run gs_${sp}_q$qt 300 python bench.py --steps 40 --warmup 5 --no-cpu-baseline --no-host-inclusive; done; done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
