@@ -113,6 +113,11 @@ for step in "$@"; do
                   python tools/prof_summary.py gpurun_out/prof_c4_$part > gpurun_out/prof_c4_${part}_summary.txt 2>&1
                 done ;;
     gsweep) for sp in 4 8 16; do for qt in 0 1; do PBF_GATHER_SPLIT=$sp PBF_GATHER_QTAB=$qt run gs_${sp}_q$qt 300 python bench.py --steps 40 --warmup 5 --no-cpu-baseline --no-host-inclusive; done; done ;;
+    selflaunch) export PBF_BENCH_DEVICE=0 PBF_BENCH_BACKEND=gloo
+                run sl_c2_n2 300 python bench.py --gpus 2 --steps 10 --warmup 3 --no-host-inclusive
+                run sl_c2_n4 300 python bench.py --gpus 4 --steps 10 --warmup 3 --no-host-inclusive
+                run sl_c5_n2 300 python bench.py --gpus 2 --config c5 --steps 3 --warmup 1 --no-host-c5
+                unset PBF_BENCH_DEVICE PBF_BENCH_BACKEND ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
