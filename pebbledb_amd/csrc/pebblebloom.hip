@@ -140,6 +140,17 @@ int probe_stage1() {
     return v;
 }
 
+// Most partition workgroups of one pipeline (PBF_PART_G overrides; default 256 = one per CU).
+// More workgroups mean fewer keys each: smaller gather key bitmaps and run tables.
+uint64_t part_max_groups() {
+    static const uint64_t v = [] {
+        const char* e = std::getenv("PBF_PART_G");
+        const long long x = e ? std::atoll(e) : 0;
+        return x > 0 ? uint64_t(std::min<long long>(x, 8192)) : uint64_t(256);
+    }();
+    return v;
+}
+
 // Tile-range splits of the ring probe's gather (PBF_GATHER_SPLIT overrides; 1 = one workgroup
 // per partition workgroup, writing the hit mask directly).
 uint32_t gather_splits() {
@@ -529,7 +540,7 @@ PartPlan plan_ring(uint32_t B, uint32_t k, uint64_t n, uint32_t rc, double share
     share = std::min(1.0, share * double(1u << sb));  // a super-tile holds 2^sb tiles
     pl.pg.sb = sb;
     pl.pg.nsup = nsup;
-    const uint64_t G0 = std::min<uint64_t>(256, std::max<uint64_t>(1, (n + kps - 1) / kps));
+    const uint64_t G0 = std::min<uint64_t>(part_max_groups(), std::max<uint64_t>(1, (n + kps - 1) / kps));
     uint64_t kpw = (n + G0 - 1) / G0;
     kpw = ((kpw + kps - 1) / kps) * kps;
     pl.pg.G = uint32_t(std::max<uint64_t>(1, (n + kpw - 1) / kpw));
@@ -556,7 +567,7 @@ PartPlan plan_partition(uint32_t B, uint32_t k, int km, uint64_t n, bool probe, 
     if (probe) kpt = std::min<uint64_t>(kpt, (kSlotMask + 1) / kPartThreads);
     const uint64_t kps = kpt * kPartThreads;
     pl.lds_part = fixed + size_t(kps) * k * per_entry;
-    const uint64_t G0 = std::min<uint64_t>(256, std::max<uint64_t>(1, (n + kps - 1) / kps));
+    const uint64_t G0 = std::min<uint64_t>(part_max_groups(), std::max<uint64_t>(1, (n + kps - 1) / kps));
     uint64_t kpw = (n + G0 - 1) / G0;
     kpw = ((kpw + kps - 1) / kps) * kps;
     pl.pg.G = uint32_t(std::max<uint64_t>(1, (n + kpw - 1) / kpw));

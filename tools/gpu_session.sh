@@ -118,6 +118,8 @@ for step in "$@"; do
                 run sl_c2_n4 300 python bench.py --gpus 4 --steps 10 --warmup 3 --no-host-inclusive
                 run sl_c5_n2 300 python bench.py --gpus 2 --config c5 --steps 3 --warmup 1 --no-host-c5
                 unset PBF_BENCH_DEVICE PBF_BENCH_BACKEND ;;
+    gsweepG) for G in ${PBF_GS:-256 512 1024}; do PBF_PART_G=$G run c3_G$G 300 python bench.py --config c3 --steps 3 --warmup 1 --no-cpu-baseline --no-host-inclusive; done
+             for G in 256 512; do PBF_PART_G=$G run c2_G$G 300 python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-host-inclusive; done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
