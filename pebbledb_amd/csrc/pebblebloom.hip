@@ -142,13 +142,16 @@ int probe_stage1() {
 
 // Most partition workgroups of one pipeline (PBF_PART_G overrides; default 256 = one per CU).
 // More workgroups mean fewer keys each: smaller gather key bitmaps and run tables.
-uint64_t part_max_groups() {
-    static const uint64_t v = [] {
+// Measured (profiles/r02/s5): the counting-sort PROBE partition prefers 512 (C3 probe 17.4 ->
+// 16.0 ms: the gather's per-workgroup key bitmap and run tables halve, more gather workgroups
+// fit a CU), the ring partition 256 (C2 probe 0.586 -> 0.604 ms at 512).
+uint64_t part_max_groups(bool sort_probe) {
+    static const long long v = [] {
         const char* e = std::getenv("PBF_PART_G");
-        const long long x = e ? std::atoll(e) : 0;
-        return x > 0 ? uint64_t(std::min<long long>(x, 8192)) : uint64_t(256);
+        return e ? std::atoll(e) : 0LL;
     }();
-    return v;
+    if (v > 0) return uint64_t(std::min<long long>(v, 8192));
+    return sort_probe ? 512 : 256;
 }
 
 // Tile-range splits of the ring probe's gather (PBF_GATHER_SPLIT overrides; 1 = one workgroup
@@ -540,7 +543,7 @@ PartPlan plan_ring(uint32_t B, uint32_t k, uint64_t n, uint32_t rc, double share
     share = std::min(1.0, share * double(1u << sb));  // a super-tile holds 2^sb tiles
     pl.pg.sb = sb;
     pl.pg.nsup = nsup;
-    const uint64_t G0 = std::min<uint64_t>(part_max_groups(), std::max<uint64_t>(1, (n + kps - 1) / kps));
+    const uint64_t G0 = std::min<uint64_t>(part_max_groups(false), std::max<uint64_t>(1, (n + kps - 1) / kps));
     uint64_t kpw = (n + G0 - 1) / G0;
     kpw = ((kpw + kps - 1) / kps) * kps;
     pl.pg.G = uint32_t(std::max<uint64_t>(1, (n + kpw - 1) / kpw));
@@ -567,7 +570,7 @@ PartPlan plan_partition(uint32_t B, uint32_t k, int km, uint64_t n, bool probe, 
     if (probe) kpt = std::min<uint64_t>(kpt, (kSlotMask + 1) / kPartThreads);
     const uint64_t kps = kpt * kPartThreads;
     pl.lds_part = fixed + size_t(kps) * k * per_entry;
-    const uint64_t G0 = std::min<uint64_t>(part_max_groups(), std::max<uint64_t>(1, (n + kps - 1) / kps));
+    const uint64_t G0 = std::min<uint64_t>(part_max_groups(probe), std::max<uint64_t>(1, (n + kps - 1) / kps));
     uint64_t kpw = (n + G0 - 1) / G0;
     kpw = ((kpw + kps - 1) / kps) * kps;
     pl.pg.G = uint32_t(std::max<uint64_t>(1, (n + kpw - 1) / kpw));
