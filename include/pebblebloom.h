@@ -166,6 +166,17 @@ int pbf_encode_data_blocks(int device, const uint8_t* keys, const uint64_t* key_
                            const uint64_t* value_offsets, uint64_t n, const uint64_t* block_first,
                            const uint64_t* block_out, uint64_t nblocks, uint8_t* out, int on_device);
 
+/* SSTableBuilder.add x n + build (src/sstable.py:224-288) in one call, for the flush of a
+ * packed run of records (host memory; offsets start at 0): one H2D of the keys, values and
+ * block plan (as for pbf_encode_data_blocks), the data blocks encoded on the device, the filter
+ * f (sized by the caller with the reference's build_from_keys_and_fp_rate expression, fp 0.001)
+ * built from the SAME device copy of the keys, and D2H of the data section into data_out
+ * (block_out[nblocks] bytes) and of the bitmap into bitmap_out (f's nb_bytes, may be NULL) —
+ * the caller points both at their slices of the SSTable file buffer.  Synchronous. */
+int pbf_build_sstable(pbf_filter_t* f, const uint8_t* keys, const uint64_t* key_offsets, const uint8_t* values,
+                      const uint64_t* value_offsets, uint64_t n, const uint64_t* block_first, const uint64_t* block_out,
+                      uint64_t nblocks, uint8_t* data_out, uint8_t* bitmap_out);
+
 /* The level key-range pre-check of LsmStorage.get (src/lsm_storage.py:171-175) for a batch:
  * out[t * ceil(n/8) + i/8] bit (i & 7) = (first_t <= key_i <= last_t), Python str order =
  * bytewise lexicographic order of the UTF-8 keys.  Bounds are 2*ntables byte strings

@@ -249,13 +249,15 @@ struct Scratch {
     uint32_t ovf_phase = 0;  // which of the two overflow counters the next build uses
     bool ovf_init = false;
     DevBuf dkeys, doffs, dout;
+    DevBuf svals, splan, ssec, serr;  // pbf_build_sstable: values + value offsets, block plan, section
     PinBuf pin[2];
     int pin_next = 0;
     hipEvent_t last = nullptr;          // completion of the last user's work
     hipStream_t last_stream = nullptr;  // ... on this stream
     bool leased = false;
     void release_all() {
-        for (DevBuf* d : {&regions, &fill, &ovf, &ovf_count, &subcnt, &rbits, &neg, &alive, &hw, &dkeys, &doffs, &dout})
+        for (DevBuf* d : {&regions, &fill, &ovf, &ovf_count, &subcnt, &rbits, &neg, &alive, &hw, &dkeys, &doffs, &dout,
+                          &svals, &splan, &ssec, &serr})
             d->release();
         pin[0].release();
         pin[1].release();
@@ -1392,7 +1394,8 @@ int pbf_scratch_bytes(int device, uint64_t* out) {
     uint64_t t = 0;
     for (Scratch* sc : pool.sets)
         for (const DevBuf* d : {&sc->regions, &sc->fill, &sc->ovf, &sc->ovf_count, &sc->subcnt, &sc->rbits, &sc->neg,
-                                &sc->alive, &sc->hw, &sc->dkeys, &sc->doffs, &sc->dout})
+                                &sc->alive, &sc->hw, &sc->dkeys, &sc->doffs, &sc->dout, &sc->svals, &sc->splan,
+                                &sc->ssec, &sc->serr})
             t += d->bytes;
     *out = t;
     return PBF_OK;
@@ -1695,6 +1698,72 @@ int pbf_encode_data_blocks(int device, const uint8_t* keys, const uint64_t* key_
     if (!on_device) HIP_TRY(hipMemcpyAsync(out, dout, out_bytes, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     if (err) return fail(PBF_ERR_INVALID, std::to_string(err) + " block(s) exceed 65536 data bytes; not written");
+    return PBF_OK;
+}
+
+int pbf_build_sstable(pbf_filter_t* f, const uint8_t* keys, const uint64_t* key_offsets, const uint8_t* values,
+                      const uint64_t* value_offsets, uint64_t n, const uint64_t* block_first, const uint64_t* block_out,
+                      uint64_t nblocks, uint8_t* data_out, uint8_t* bitmap_out) {
+    LOCK(f);
+    int rc = enter(f);
+    if (rc) return rc;
+    if (n == 0 || nblocks == 0) return fail(PBF_ERR_INVALID, "an SSTable needs at least one record");
+    if (!keys || !key_offsets || !values || !value_offsets || !block_first || !block_out || !data_out)
+        return fail(PBF_ERR_INVALID, "null pointer");
+    if (key_offsets[0] != 0 || value_offsets[0] != 0) return fail(PBF_ERR_INVALID, "offsets must start at 0");
+    // the host plan is checked as in pbf_encode_data_blocks
+    if (block_first[0] != 0 || block_first[nblocks] != n || block_out[0] != 0)
+        return fail(PBF_ERR_INVALID, "block plan must cover records [0, n) from byte 0");
+    for (uint64_t b = 0; b < nblocks; ++b) {
+        const uint64_t r0 = block_first[b], r1 = block_first[b + 1];
+        if (r1 < r0) return fail(PBF_ERR_INVALID, "block plan not monotonic");
+        const uint64_t dl = (key_offsets[r1] - key_offsets[r0]) + (value_offsets[r1] - value_offsets[r0]) + 8 * (r1 - r0);
+        if (dl > kMaxBlockData) return fail(PBF_ERR_INVALID, "a block's records exceed 65536 bytes");
+        if (block_out[b + 1] - block_out[b] != dl + 2 * (r1 - r0) + 2)
+            return fail(PBF_ERR_INVALID, "block_out does not match the blocks' encoded sizes");
+    }
+    HIP_TRY(allow_lds(k_encode_blocks, kEncodeLds));
+    LEASE(f);
+    Scratch* sc = f->sc;
+    hipStream_t s = f->stream;
+    const uint64_t kb = key_offsets[n], vb = value_offsets[n], out_bytes = block_out[nblocks];
+    HIP_TRY(sc->dkeys.ensure(((kb + 15) & ~uint64_t(15)) + 32));
+    HIP_TRY(sc->doffs.ensure((n + 1) * 8));
+    HIP_TRY(sc->svals.ensure(((vb + 15) & ~uint64_t(15)) + 32 + (n + 1) * 8));
+    HIP_TRY(sc->splan.ensure(2 * (nblocks + 1) * 8));
+    HIP_TRY(sc->ssec.ensure(out_bytes + 32));
+    HIP_TRY(sc->serr.ensure(4));
+    auto* dk = static_cast<uint8_t*>(sc->dkeys.p);
+    auto* dko = static_cast<uint64_t*>(sc->doffs.p);
+    auto* dv = static_cast<uint8_t*>(sc->svals.p);
+    auto* dvo = reinterpret_cast<uint64_t*>(dv + ((vb + 15) & ~uint64_t(15)) + 32);
+    auto* dbf = static_cast<uint64_t*>(sc->splan.p);
+    auto* dbo = dbf + nblocks + 1;
+    // one H2D of the packed records; the data blocks and the filter are both built from it
+    if (kb) HIP_TRY(hipMemcpyAsync(dk, keys, kb, hipMemcpyHostToDevice, s));
+    if (vb) HIP_TRY(hipMemcpyAsync(dv, values, vb, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(dko, key_offsets, (n + 1) * 8, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(dvo, value_offsets, (n + 1) * 8, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(dbf, block_first, (nblocks + 1) * 8, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(dbo, block_out, (nblocks + 1) * 8, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemsetAsync(sc->serr.p, 0, 4, s));
+    k_encode_blocks<<<uint32_t(nblocks), 512, kEncodeLds, s>>>(dk, dko, dv, dvo, dbf, dbo, static_cast<uint8_t*>(sc->ssec.p),
+                                                               static_cast<unsigned int*>(sc->serr.p));
+    CHECK_LAUNCH();
+    if (f->k > 0) {  // SSTableBuilder.build's filter over every key (sstable.py:274)
+        rc = add_device(f, make_batch(dk, dko, 0, n));
+        if (rc) return rc;
+    }
+    unsigned int err = 0;
+    HIP_TRY(hipMemcpyAsync(&err, sc->serr.p, 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(data_out, sc->ssec.p, out_bytes, hipMemcpyDeviceToHost, s));
+    if (bitmap_out) {
+        rc = materialise(f);
+        if (rc) return rc;
+        HIP_TRY(hipMemcpyAsync(bitmap_out, f->bitmap, f->nb_bytes, hipMemcpyDeviceToHost, s));
+    }
+    WAIT(f);
+    if (err) return fail(PBF_ERR_INVALID, std::to_string(err) + " block(s) exceed 65536 data bytes");
     return PBF_OK;
 }
 

@@ -111,11 +111,16 @@ def build_sstable(keys, values=None, block_size: int = BLOCK_SIZE, fp_rate: floa
     """The bytes SSTableBuilder(block_size=block_size) writes after add(k, v) for every record
     and build() (sstable.py:270-288), plus the meta blocks and the device BloomFilter.
 
-    `keys` is either a PackedRecords (values None) — e.g. ``PackedRecords.from_iter(
-    MemTableIterator(memtable))``, the flush path with no per-record Python — or list[str] with
-    `values` list[bytes]."""
+    `keys` is either a PackedRecords (values None) — e.g. ``PackedRecords.from_encoded(
+    iter(memtable.map))``, the flush path with no per-record Python — or list[str] with
+    `values` list[bytes].  The device work is ONE call (``pbf_build_sstable``): the records go
+    to the GPU once, the data blocks and the filter (build_from_keys_and_fp_rate's sizing,
+    bloom_filter.py:109-114, fp 0.001 as sstable.py:274) are both built from that copy, and the
+    data section and the bitmap are copied straight into their slices of the file buffer."""
+    from math import ceil, log
+
     from .bloom_filter import BloomFilter, _default_device
-    from .sstable_bloom import encode_sstable
+    from .sstable_bloom import TRAILER, sstable_size
 
     dev = _default_device if device is None else int(device)
     if isinstance(keys, PackedRecords):
@@ -128,8 +133,31 @@ def build_sstable(keys, values=None, block_size: int = BLOCK_SIZE, fp_rate: floa
         vals, vo = pack_values(values)
     if len(vo) - 1 != pk.n:
         raise ValueError("keys and values differ in length")
-    bf_first, bo = plan_blocks(key_offsets(pk), vo, block_size)
-    data = encode_data_blocks(pk, vals, vo, bf_first, bo, dev)
+    ko = np.ascontiguousarray(key_offsets(pk), dtype=np.uint64)
+    vo = np.ascontiguousarray(vo, dtype=np.uint64)
+    bf_first, bo = plan_blocks(ko, vo, block_size)
     meta, metas = meta_blocks(keys if isinstance(keys, list) else pk, bf_first, bo)
-    bloom = BloomFilter.build_from_keys_and_fp_rate(pk, fp_rate, device=dev)
-    return encode_sstable(memoryview(data), meta, bloom), metas, bloom
+    n = pk.n
+    m = (-n * log(fp_rate)) / (log(2) ** 2)  # bloom_filter.py:109-114, same expression order
+    nb_bytes, k = ceil(m / 8), round((m / n) * log(2))
+    if not 0 <= k <= 255:
+        raise struct.error("ubyte format requires 0 <= number <= 255")  # SSTableEncoding -> to_bytes
+    bloom = BloomFilter(nb_bytes, k, device=dev)
+    data_len = int(bo[-1])
+    if data_len + len(meta) > 0x7FFFFFFF:
+        raise struct.error("'i' format requires -2147483648 <= number <= 2147483647")
+    out = bytearray(sstable_size(data_len, len(meta), nb_bytes))
+    buf = np.frombuffer(out, dtype=np.uint8)
+    bloom_off = data_len + len(meta)
+    kbytes = pk.data if pk.data.size else np.zeros(1, np.uint8)
+    vbytes = vals if vals.size else np.zeros(1, np.uint8)
+    vp = ctypes.c_void_p
+    rc = _native.lib().pbf_build_sstable(bloom.handle, vp(kbytes.ctypes.data), vp(ko.ctypes.data),
+                                         vp(vbytes.ctypes.data), vp(vo.ctypes.data), n, vp(bf_first.ctypes.data),
+                                         vp(bo.ctypes.data), len(bf_first) - 1, vp(buf.ctypes.data),
+                                         vp(buf.ctypes.data + bloom_off))
+    _native.check(rc, "pbf_build_sstable")
+    out[data_len:bloom_off] = meta
+    out[bloom_off + nb_bytes] = k
+    struct.pack_into("ii", out, len(out) - TRAILER, data_len, bloom_off)
+    return out, metas, bloom
