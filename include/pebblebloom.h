@@ -177,6 +177,13 @@ int pbf_build_sstable(pbf_filter_t* f, const uint8_t* keys, const uint64_t* key_
                       const uint64_t* value_offsets, uint64_t n, const uint64_t* block_first, const uint64_t* block_out,
                       uint64_t nblocks, uint8_t* data_out, uint8_t* bitmap_out);
 
+/* DataBlockBuilder's greedy blocks (src/blocks.py:78-95, sstable.py:224-244) over n records
+ * whose key / value bytes are given by their offsets: block_first[0..nblocks] record indices,
+ * block_out[0..nblocks] byte offsets of the encoded blocks (both sized n+1 by the caller);
+ * *nblocks receives the count.  Host-side planning for pbf_build_sstable. */
+int pbf_plan_blocks(const uint64_t* key_offsets, const uint64_t* value_offsets, uint64_t n, uint64_t block_size,
+                    uint64_t* block_first, uint64_t* block_out, uint64_t* nblocks);
+
 /* The level key-range pre-check of LsmStorage.get (src/lsm_storage.py:171-175) for a batch:
  * out[t * ceil(n/8) + i/8] bit (i & 7) = (first_t <= key_i <= last_t), Python str order =
  * bytewise lexicographic order of the UTF-8 keys.  Bounds are 2*ntables byte strings

@@ -59,6 +59,7 @@ SIGNATURES = {
     "pbf_scratch_bytes": (_int, [_int, ctypes.POINTER(_u64)]),
     "pbf_encode_data_blocks": (_int, [_int, _u8p, _vp, _u8p, _vp, _u64, _vp, _vp, _u64, _u8p, _int]),
     "pbf_build_sstable": (_int, [_vp, _u8p, _vp, _u8p, _vp, _u64, _vp, _vp, _u64, _u8p, _u8p]),
+    "pbf_plan_blocks": (_int, [_vp, _vp, _u64, _u64, _vp, _vp, ctypes.POINTER(_u64)]),
     "pbf_key_range_mask": (_int, [_int, _vp, _u8p, _vp, _u32, _u64, _u8p, _vp, _u32, _u8p, _int]),
     "pbf_gen_splitmix_hex": (_int, [_int, _vp, _u8p, _u64, _u64, _u64]),
     "pbf_gen_varlen": (_int, [_int, _vp, _u8p, _vp, _u64, _u64, _u64]),

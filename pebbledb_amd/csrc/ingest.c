@@ -274,12 +274,20 @@ static PyObject* py_pack_encoded(PyObject* self, PyObject* args) {
     PyObject* item;
     while ((item = next_item(seq, it, &idx))) {
         Py_buffer view;
-        if (PyObject_GetBuffer(item, &view, PyBUF_SIMPLE)) {
-            Py_DECREF(item);
-            goto fail;
+        view.obj = NULL;
+        const unsigned char* d;
+        size_t L;
+        if (PyBytes_CheckExact(item)) {  // the memtable's records are bytes: no buffer request
+            d = (const unsigned char*)PyBytes_AS_STRING(item);
+            L = (size_t)PyBytes_GET_SIZE(item);
+        } else {
+            if (PyObject_GetBuffer(item, &view, PyBUF_SIMPLE)) {
+                Py_DECREF(item);
+                goto fail;
+            }
+            d = (const unsigned char*)view.buf;
+            L = (size_t)view.len;
         }
-        const unsigned char* d = (const unsigned char*)view.buf;
-        const size_t L = (size_t)view.len;
         int32_t ks, vs;
         int rc = -1;
         // Record._from_bytes, step by step: struct.unpack needs 4 bytes; the key and value
@@ -324,7 +332,7 @@ static PyObject* py_pack_encoded(PyObject* self, PyObject* args) {
         // struct.unpack("i", ...) of fewer than 4 bytes: struct.error, as in the reference
         PyErr_SetString(s_struct_error, "unpack requires a buffer of 4 bytes");
     out:
-        PyBuffer_Release(&view);
+        if (view.obj) PyBuffer_Release(&view);
         Py_DECREF(item);
         if (rc) goto fail;
         ++n;

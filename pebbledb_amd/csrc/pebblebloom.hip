@@ -1739,6 +1739,28 @@ int pbf_build_sstable(pbf_filter_t* f, const uint8_t* keys, const uint64_t* key_
     auto* dvo = reinterpret_cast<uint64_t*>(dv + ((vb + 15) & ~uint64_t(15)) + 32);
     auto* dbf = static_cast<uint64_t*>(sc->splan.p);
     auto* dbo = dbf + nblocks + 1;
+    // Page-lock the large host spans for the duration of the call so the copies are direct DMA
+    // (pageable copies go through the runtime's staging at a fraction of the rate); spans that
+    // are already pinned, or cannot be registered, are copied as they are.
+    std::vector<void*> registered;
+    auto lock_span = [&](const void* p, uint64_t bytes) {
+        if (bytes < (uint64_t(4) << 20) || is_pinned_host(p)) return;
+        if (hipHostRegister(const_cast<void*>(p), bytes, hipHostRegisterDefault) == hipSuccess)
+            registered.push_back(const_cast<void*>(p));
+        else
+            (void)hipGetLastError();
+    };
+    struct Unregister {
+        std::vector<void*>& v;
+        ~Unregister() {
+            for (void* p : v) (void)hipHostUnregister(p);
+        }
+    } unreg{registered};
+    lock_span(keys, kb);
+    lock_span(values, vb);
+    lock_span(key_offsets, (n + 1) * 8);
+    lock_span(value_offsets, (n + 1) * 8);
+    lock_span(data_out, out_bytes);
     // one H2D of the packed records; the data blocks and the filter are both built from it
     if (kb) HIP_TRY(hipMemcpyAsync(dk, keys, kb, hipMemcpyHostToDevice, s));
     if (vb) HIP_TRY(hipMemcpyAsync(dv, values, vb, hipMemcpyHostToDevice, s));
@@ -1764,6 +1786,39 @@ int pbf_build_sstable(pbf_filter_t* f, const uint8_t* keys, const uint64_t* key_
     }
     WAIT(f);
     if (err) return fail(PBF_ERR_INVALID, std::to_string(err) + " block(s) exceed 65536 data bytes");
+    return PBF_OK;
+}
+
+int pbf_plan_blocks(const uint64_t* key_offsets, const uint64_t* value_offsets, uint64_t n, uint64_t block_size,
+                    uint64_t* block_first, uint64_t* block_out, uint64_t* nblocks) {
+    if (!key_offsets || !value_offsets || !block_first || !block_out || !nblocks) return fail(PBF_ERR_INVALID, "null pointer");
+    if (n == 0) return fail(PBF_ERR_INVALID, "an SSTable needs at least one record");
+    if (block_size == 0 || block_size > kMaxBlockData) return fail(PBF_ERR_INVALID, "block_size must be in (0, 65536]");
+    // DataBlockBuilder.add (blocks.py:78-95): a record joins the open block iff the block's
+    // record bytes stay <= block_size; a record larger than a block cannot be placed (the
+    // reference would drop it, blocks.py:84-85)
+    uint64_t nb = 0, used = 0, out = 0, cnt = 0;
+    block_first[0] = 0;
+    block_out[0] = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint64_t sz = (key_offsets[i + 1] - key_offsets[i]) + (value_offsets[i + 1] - value_offsets[i]) + 8;
+        if (sz > block_size) return fail(PBF_ERR_INVALID, "a record is larger than block_size");
+        if (cnt && used + sz > block_size) {
+            out += used + 2 * cnt + 2;
+            ++nb;
+            block_first[nb] = i;
+            block_out[nb] = out;
+            used = 0;
+            cnt = 0;
+        }
+        used += sz;
+        ++cnt;
+    }
+    out += used + 2 * cnt + 2;
+    ++nb;
+    block_first[nb] = n;
+    block_out[nb] = out;
+    *nblocks = nb;
     return PBF_OK;
 }
 

@@ -44,7 +44,8 @@ def pack_values(values) -> tuple[np.ndarray, np.ndarray]:
 def key_offsets(pk: PackedKeys) -> np.ndarray:
     if pk.offsets is not None:
         return pk.offsets
-    return np.arange(pk.n + 1, dtype=np.uint64) * np.uint64(pk.key_len)
+    return np.arange(0, (pk.n + 1) * pk.key_len, max(pk.key_len, 1), dtype=np.uint64)[:pk.n + 1] \
+        if pk.key_len else np.zeros(pk.n + 1, dtype=np.uint64)
 
 
 def plan_blocks(ko: np.ndarray, vo: np.ndarray, block_size: int = BLOCK_SIZE) -> tuple[np.ndarray, np.ndarray]:
@@ -73,6 +74,27 @@ def plan_blocks(ko: np.ndarray, vo: np.ndarray, block_size: int = BLOCK_SIZE) ->
     bo = np.zeros(len(bf), dtype=np.uint64)
     np.cumsum(data_len + 2 * cnt + 2, out=bo[1:])
     return bf, bo
+
+
+def plan_blocks_native(ko: np.ndarray, vo: np.ndarray, block_size: int = BLOCK_SIZE) -> tuple[np.ndarray, np.ndarray]:
+    """plan_blocks by the C planner (pbf_plan_blocks: one pass over the record sizes)."""
+    n = len(ko) - 1
+    if n <= 0:
+        raise ValueError("an SSTable needs at least one record (the reference fails in MetaBlock.to_bytes)")
+    if not 0 < block_size <= 65_536:
+        raise ValueError("block_size must be in (0, 65536]: DataBlock offsets are u16 (blocks.py:34)")
+    ko = np.ascontiguousarray(ko, dtype=np.uint64)
+    vo = np.ascontiguousarray(vo, dtype=np.uint64)
+    bf = np.empty(n + 1, dtype=np.uint64)
+    bo = np.empty(n + 1, dtype=np.uint64)
+    nb = ctypes.c_uint64(0)
+    vp = ctypes.c_void_p
+    rc = _native.lib().pbf_plan_blocks(vp(ko.ctypes.data), vp(vo.ctypes.data), n, block_size, vp(bf.ctypes.data),
+                                       vp(bo.ctypes.data), ctypes.byref(nb))
+    if rc == _native.PBF_ERR_INVALID and "larger than block_size" in _native.lib().pbf_last_error().decode():
+        raise ValueError("a record is larger than block_size (the reference would drop it, blocks.py:84-85)")
+    _native.check(rc, "pbf_plan_blocks")
+    return bf[:nb.value + 1].copy(), bo[:nb.value + 1].copy()
 
 
 def encode_data_blocks(pk: PackedKeys, vals: np.ndarray, vo: np.ndarray, block_first: np.ndarray,
@@ -113,7 +135,8 @@ def build_sstable(keys, values=None, block_size: int = BLOCK_SIZE, fp_rate: floa
 
     `keys` is either a PackedRecords (values None) — e.g. ``PackedRecords.from_encoded(
     iter(memtable.map))``, the flush path with no per-record Python — or list[str] with
-    `values` list[bytes].  The device work is ONE call (``pbf_build_sstable``): the records go
+    `values` list[bytes].  Returns (file bytes as a uint8 numpy array, meta blocks, filter).
+    The device work is ONE call (``pbf_build_sstable``): the records go
     to the GPU once, the data blocks and the filter (build_from_keys_and_fp_rate's sizing,
     bloom_filter.py:109-114, fp 0.001 as sstable.py:274) are both built from that copy, and the
     data section and the bitmap are copied straight into their slices of the file buffer."""
@@ -135,7 +158,7 @@ def build_sstable(keys, values=None, block_size: int = BLOCK_SIZE, fp_rate: floa
         raise ValueError("keys and values differ in length")
     ko = np.ascontiguousarray(key_offsets(pk), dtype=np.uint64)
     vo = np.ascontiguousarray(vo, dtype=np.uint64)
-    bf_first, bo = plan_blocks(ko, vo, block_size)
+    bf_first, bo = plan_blocks_native(ko, vo, block_size)
     meta, metas = meta_blocks(keys if isinstance(keys, list) else pk, bf_first, bo)
     n = pk.n
     m = (-n * log(fp_rate)) / (log(2) ** 2)  # bloom_filter.py:109-114, same expression order
@@ -146,8 +169,10 @@ def build_sstable(keys, values=None, block_size: int = BLOCK_SIZE, fp_rate: floa
     data_len = int(bo[-1])
     if data_len + len(meta) > 0x7FFFFFFF:
         raise struct.error("'i' format requires -2147483648 <= number <= 2147483647")
-    out = bytearray(sstable_size(data_len, len(meta), nb_bytes))
-    buf = np.frombuffer(out, dtype=np.uint8)
+    # the file buffer: every byte is written below (data and bitmap by the device, the rest
+    # here), so it is not zero-filled first (a 76 MB bytearray's fill alone cost 14 ms)
+    out = np.empty(sstable_size(data_len, len(meta), nb_bytes), dtype=np.uint8)
+    buf = out
     bloom_off = data_len + len(meta)
     kbytes = pk.data if pk.data.size else np.zeros(1, np.uint8)
     vbytes = vals if vals.size else np.zeros(1, np.uint8)
@@ -157,7 +182,7 @@ def build_sstable(keys, values=None, block_size: int = BLOCK_SIZE, fp_rate: floa
                                          vp(bo.ctypes.data), len(bf_first) - 1, vp(buf.ctypes.data),
                                          vp(buf.ctypes.data + bloom_off))
     _native.check(rc, "pbf_build_sstable")
-    out[data_len:bloom_off] = meta
+    out[data_len:bloom_off] = np.frombuffer(meta, dtype=np.uint8)
     out[bloom_off + nb_bytes] = k
-    struct.pack_into("ii", out, len(out) - TRAILER, data_len, bloom_off)
+    out[len(out) - TRAILER:] = np.frombuffer(struct.pack("ii", data_len, bloom_off), dtype=np.uint8)
     return out, metas, bloom

@@ -73,3 +73,24 @@ def test_planner_rejects_what_the_reference_mishandles():
 def test_record_key_size_counts_characters():
     # record.py:24 — key_size = len(str): 4 for "clé!" although it is 5 UTF-8 bytes
     assert so.record_bytes("clé!", b"v")[:4] == (4).to_bytes(4, "little")
+
+
+def test_native_block_planner_equals_reference_rule():
+    """pbf_plan_blocks (host C, no GPU) == the numpy restatement of DataBlockBuilder.add's rule
+    (blocks.py:78-95) on random record sizes, exactly-full blocks and single-record blocks."""
+    from pebbledb_amd.sstable_data import plan_blocks, plan_blocks_native
+    rng = np.random.default_rng(1)
+    for n, bs, maxk, maxv in ((1, 64, 8, 8), (5000, 256, 30, 100), (20000, 65536, 64, 3000), (300, 100, 40, 52)):
+        kl = rng.integers(0, maxk + 1, n)
+        vl = rng.integers(0, maxv + 1, n)
+        kl = np.minimum(kl, bs - 8)
+        vl = np.minimum(vl, bs - 8 - kl)
+        ko = np.concatenate([[0], np.cumsum(kl)]).astype(np.uint64)
+        vo = np.concatenate([[0], np.cumsum(vl)]).astype(np.uint64)
+        a, b = plan_blocks(ko, vo, bs)
+        c, d = plan_blocks_native(ko, vo, bs)
+        assert np.array_equal(a, c) and np.array_equal(b, d), (n, bs)
+    ko = np.array([0, 10], np.uint64)
+    vo = np.array([0, 60], np.uint64)
+    with pytest.raises(ValueError):
+        plan_blocks_native(ko, vo, 64)  # 10 + 60 + 8 > 64
