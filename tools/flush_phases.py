@@ -11,7 +11,7 @@ import numpy as np
 sys.path.insert(0, ".")
 from pebbledb_amd import BloomFilter, _native  # noqa: E402
 from pebbledb_amd.keys import PackedRecords  # noqa: E402
-from pebbledb_amd.sstable_data import key_offsets, meta_blocks, plan_blocks  # noqa: E402
+from pebbledb_amd.sstable_data import key_offsets, meta_blocks, plan_blocks_native  # noqa: E402
 from pebbledb_amd.sstable_bloom import sstable_size  # noqa: E402
 
 n, vlen = 1_000_000, 48
@@ -27,7 +27,7 @@ for rep in range(3):
     pk, vb, vo = pr.keys, pr.values, pr.value_offsets
     ko = np.ascontiguousarray(key_offsets(pk), dtype=np.uint64)
     t["key_offsets"] = time.perf_counter()
-    bf, bo = plan_blocks(ko, vo, 65536)
+    bf, bo = plan_blocks_native(ko, vo, 65536)
     t["plan"] = time.perf_counter()
     meta, metas = meta_blocks(pk, bf, bo)
     t["meta"] = time.perf_counter()
@@ -36,16 +36,16 @@ for rep in range(3):
     bloom = BloomFilter(nb, k)
     t["filter_create"] = time.perf_counter()
     data_len = int(bo[-1])
-    out = bytearray(sstable_size(data_len, len(meta), nb))
+    out = np.empty(sstable_size(data_len, len(meta), nb), dtype=np.uint8)
     t["file_alloc"] = time.perf_counter()
-    buf = np.frombuffer(out, dtype=np.uint8)
+    buf = out
     vp = ctypes.c_void_p
     _native.check(_native.lib().pbf_build_sstable(bloom.handle, vp(pk.data.ctypes.data), vp(ko.ctypes.data),
                                                   vp(vb.ctypes.data), vp(vo.ctypes.data), n, vp(bf.ctypes.data),
                                                   vp(bo.ctypes.data), len(bf) - 1, vp(buf.ctypes.data),
                                                   vp(buf.ctypes.data + data_len + len(meta))), "build")
     t["device_build"] = time.perf_counter()
-    out[data_len:data_len + len(meta)] = meta
+    out[data_len:data_len + len(meta)] = np.frombuffer(meta, dtype=np.uint8)
     t["assemble"] = time.perf_counter()
     prev = t0
     parts = []
