@@ -332,6 +332,72 @@ bool event_done(hipEvent_t e) {
     return r == hipSuccess;
 }
 
+// Bitmap allocations (bitmap words + the popcount slot) are recycled per device and size:
+// an LSM creates a filter per flushed / compacted SSTable and drops it with the SSTable, and a
+// hipMalloc + hipFree pair cost milliseconds per filter.  At most PBF_BITMAP_CACHE_MB (default
+// 1024) of freed bitmaps are kept; pbf_trim releases them.
+size_t bitmap_alloc_bytes(uint64_t alloc_words) { return size_t(alloc_words) * 4 + 16; }
+
+struct BitmapCache {
+    std::mutex mu;
+    std::map<std::pair<int, size_t>, std::vector<void*>> free;
+    size_t bytes = 0;
+};
+BitmapCache& bitmap_cache() {
+    static BitmapCache c;
+    return c;
+}
+size_t bitmap_cache_cap() {
+    static const size_t v = [] {
+        const char* e = std::getenv("PBF_BITMAP_CACHE_MB");
+        const long long x = e ? std::atoll(e) : -1;
+        return x >= 0 ? size_t(x) << 20 : size_t(1024) << 20;
+    }();
+    return v;
+}
+
+hipError_t bitmap_alloc(int device, size_t bytes, void** out) {
+    BitmapCache& c = bitmap_cache();
+    {
+        std::lock_guard<std::mutex> lock(c.mu);
+        auto it = c.free.find({device, bytes});
+        if (it != c.free.end() && !it->second.empty()) {
+            *out = it->second.back();
+            it->second.pop_back();
+            c.bytes -= bytes;
+            return hipSuccess;
+        }
+    }
+    return hipMalloc(out, bytes);
+}
+
+// The caller has synchronised the filter's stream (no queued work reads the buffer).
+void bitmap_release(int device, size_t bytes, void* p) {
+    BitmapCache& c = bitmap_cache();
+    {
+        std::lock_guard<std::mutex> lock(c.mu);
+        if (c.bytes + bytes <= bitmap_cache_cap()) {
+            c.free[{device, bytes}].push_back(p);
+            c.bytes += bytes;
+            return;
+        }
+    }
+    (void)hipFree(p);
+}
+
+void bitmap_cache_trim(int device) {
+    BitmapCache& c = bitmap_cache();
+    std::lock_guard<std::mutex> lock(c.mu);
+    for (auto& kv : c.free) {
+        if (kv.first.first != device) continue;
+        for (void* p : kv.second) {
+            (void)hipFree(p);
+            c.bytes -= kv.first.second;
+        }
+        kv.second.clear();
+    }
+}
+
 // Streams are per device, created once and dealt round-robin to filters (PBF_STREAMS, default
 // 8): creating a HIP stream per filter cost milliseconds per SSTable (measured 8-14 ms of a
 // 1M-record flush), and filters sharing a stream only order their work.
@@ -1355,8 +1421,12 @@ int pbf_create(int device, uint64_t nb_bytes, uint32_t nb_hash_functions, pbf_fi
     if (tm.nbuckets > 8192) f->tiled_ok = false;  // LDS budget of k_part
     f->tm = tm;
     hipError_t e = pooled_stream(device, &f->stream);
-    if (e == hipSuccess) e = hipMalloc(&f->bitmap, f->alloc_words * 4);
-    if (e == hipSuccess) e = hipMalloc(&f->dpop, 8);
+    if (e == hipSuccess) {
+        void* p = nullptr;
+        e = bitmap_alloc(device, bitmap_alloc_bytes(f->alloc_words), &p);
+        f->bitmap = static_cast<uint32_t*>(p);
+        if (e == hipSuccess) f->dpop = reinterpret_cast<uint64_t*>(f->bitmap + f->alloc_words);
+    }
     // The tiled build writes every reachable word itself; the unreachable middle of a
     // m > 2^32 filter is zeroed once here.  Otherwise start from an explicit zero bitmap.
     if (e == hipSuccess) {
@@ -1392,8 +1462,7 @@ int pbf_destroy(pbf_filter_t* f) {
         for (Scratch* sc : pool.sets)
             if (sc->last_stream == f->stream) sc->last_stream = nullptr;
     }
-    if (f->bitmap) (void)hipFree(f->bitmap);
-    if (f->dpop) (void)hipFree(f->dpop);
+    if (f->bitmap) bitmap_release(f->device, bitmap_alloc_bytes(f->alloc_words), f->bitmap);
     if (f->ev) (void)hipEventDestroy(f->ev);
     delete f;  // the stream belongs to the device's pool
     return PBF_OK;
@@ -1401,6 +1470,7 @@ int pbf_destroy(pbf_filter_t* f) {
 
 int pbf_trim(int device) {
     HIP_TRY(hipSetDevice(device));
+    bitmap_cache_trim(device);
     DevicePool& pool = device_pool(device);
     std::lock_guard<std::mutex> lock(pool.mu);
     for (Scratch* sc : pool.sets) {

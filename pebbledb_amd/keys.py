@@ -88,9 +88,10 @@ def varlen_keys(seed: int, start: int, n: int) -> tuple[np.ndarray, np.ndarray]:
 class PackedKeys:
     """A batch of keys in the boundary layout. ``key_len`` > 0 ⇒ fixed-width, offsets None."""
 
-    __slots__ = ("data", "offsets", "n", "key_len")
+    __slots__ = ("data", "offsets", "n", "key_len", "_ko")
 
     def __init__(self, data: np.ndarray, n: int, key_len: int = 0, offsets: np.ndarray | None = None):
+        self._ko = None  # the packer's offsets of a fixed-width batch (sstable_data.key_offsets)
         self.data = np.ascontiguousarray(data, dtype=np.uint8).reshape(-1)
         self.n = int(n)
         self.key_len = int(key_len)
@@ -139,7 +140,9 @@ class PackedKeys:
     def _from_packed(cls, kb, ko, n, lo, hi) -> "PackedKeys":
         data = np.frombuffer(kb, dtype=np.uint8) if len(kb) else np.zeros(0, np.uint8)
         if n and lo == hi and lo > 0:
-            return cls(data, n, key_len=int(lo))
+            pk = cls(data, n, key_len=int(lo))
+            pk._ko = np.frombuffer(ko, dtype=np.uint64)
+            return pk
         return cls(data, n, key_len=0, offsets=np.frombuffer(ko, dtype=np.uint64))
 
     def key(self, i: int) -> bytes:

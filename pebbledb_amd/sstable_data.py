@@ -44,6 +44,8 @@ def pack_values(values) -> tuple[np.ndarray, np.ndarray]:
 def key_offsets(pk: PackedKeys) -> np.ndarray:
     if pk.offsets is not None:
         return pk.offsets
+    if pk._ko is not None:
+        return pk._ko
     return np.arange(0, (pk.n + 1) * pk.key_len, max(pk.key_len, 1), dtype=np.uint64)[:pk.n + 1] \
         if pk.key_len else np.zeros(pk.n + 1, dtype=np.uint64)
 
