@@ -19,9 +19,12 @@ rng = np.random.default_rng(0)
 vals = rng.integers(0, 256, n * vlen, dtype=np.uint8).tobytes()
 enc = [struct.pack("i", 16) + format(i, "016x").encode() + struct.pack("i", vlen) + vals[i * vlen:(i + 1) * vlen]
        for i in range(n)]
+state = {}
 for rep in range(3):
     t = {}
     t0 = time.perf_counter()
+    state.clear()  # drop the previous rep's records, filter and file first (freeing is timed here)
+    t["free_previous"] = time.perf_counter()
     pr = PackedRecords.from_encoded(enc)
     t["pack"] = time.perf_counter()
     pk, vb, vo = pr.keys, pr.values, pr.value_offsets
@@ -35,6 +38,9 @@ for rep in range(3):
     nb, k = ceil(m / 8), round((m / n) * log(2))
     bloom = BloomFilter(nb, k)
     t["filter_create"] = time.perf_counter()
+    state.update(pr=pr, pk=pk, vb=vb, vo=vo, ko=ko, bloom=bloom)
+    del pr, pk, vb, vo, ko, bloom
+    pk, vb, vo, ko, bloom = state["pk"], state["vb"], state["vo"], state["ko"], state["bloom"]
     data_len = int(bo[-1])
     out = np.empty(sstable_size(data_len, len(meta), nb), dtype=np.uint8)
     t["file_alloc"] = time.perf_counter()
@@ -47,6 +53,8 @@ for rep in range(3):
     t["device_build"] = time.perf_counter()
     out[data_len:data_len + len(meta)] = np.frombuffer(meta, dtype=np.uint8)
     t["assemble"] = time.perf_counter()
+    state["out"] = out
+    del out, pk, vb, vo, ko, bloom, buf
     prev = t0
     parts = []
     for name, v in t.items():
