@@ -687,9 +687,15 @@ def main():
 
     torch.cuda.set_device(local)
     if world > 1:
+        # RCCL carries only the timing plumbing (barrier, max over ranks): the data path has no
+        # collective.  If it cannot start, the run goes on over gloo and says so.
         backend = os.environ.get("PBF_BENCH_BACKEND", "nccl")
         if backend == "nccl":
-            dist.init_process_group(backend="nccl", init_method="env://", device_id=torch.device("cuda", local))
+            try:
+                dist.init_process_group(backend="nccl", init_method="env://", device_id=torch.device("cuda", local))
+            except Exception as e:  # noqa: BLE001 - reported, then the gloo rendezvous
+                print(f"rank {rank}: RCCL process group failed ({e!r}); timing plumbing over gloo", file=sys.stderr)
+                dist.init_process_group(backend="gloo", init_method="env://")
         else:
             dist.init_process_group(backend=backend, init_method="env://")
 

@@ -78,6 +78,8 @@ int pbf_clear(pbf_filter_t* f);
 /* BloomFilter.add for a batch of keys (bloom_filter.py:60-65): ORs k bits per key. */
 int pbf_add_fixed(pbf_filter_t* f, const uint8_t* keys, uint32_t key_len, uint64_t n, int keys_on_device);
 int pbf_add(pbf_filter_t* f, const uint8_t* keys, const uint64_t* offsets, uint64_t n, int keys_on_device);
+/* The same call under SURVEY.md §8b's name. */
+int pbf_build(pbf_filter_t* f, const uint8_t* keys, const uint64_t* offsets, uint64_t n, int keys_on_device);
 
 /* BloomFilter.may_contain for a batch (bloom_filter.py:67-74).  hitmask receives ceil(n/8)
  * bytes, LSB-first: bit (i & 7) of hitmask[i >> 3] = may_contain(key i).  The hitmask pointer
@@ -107,6 +109,10 @@ int pbf_probe_multi(pbf_filter_t* const* filters, uint32_t nfilters, const uint8
  * hit byte comes back the same way (one launch, no copies, no allocation after the first call
  * on a thread). */
 int pbf_may_contain(pbf_filter_t* f, const uint8_t* key, uint64_t len, int* out);
+
+/* mmh3.hash(key, seed) (bloom_filter.py:46: MurmurHash3_x86_32, signed int32) of one host key
+ * of at most 4096 bytes, computed on `device` (one launch). */
+int pbf_murmur3_x86_32(int device, const uint8_t* key, uint64_t len, uint32_t seed, int32_t* out);
 
 /* The k bit indices of each key, BloomFilter._hash (bloom_filter.py:38-49): out[i*k + s] =
  * mmh3.hash(key_i, s) % bits_size (Python floor-mod).  out is host or device memory as

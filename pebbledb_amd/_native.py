@@ -36,6 +36,8 @@ SIGNATURES = {
     "pbf_clear": (_int, [_vp]),
     "pbf_add_fixed": (_int, [_vp, _u8p, _u32, _u64, _int]),
     "pbf_add": (_int, [_vp, _u8p, _vp, _u64, _int]),
+    "pbf_build": (_int, [_vp, _u8p, _vp, _u64, _int]),
+    "pbf_murmur3_x86_32": (_int, [_int, ctypes.c_char_p, _u64, _u32, ctypes.POINTER(ctypes.c_int32)]),
     "pbf_probe_fixed": (_int, [_vp, _u8p, _u32, _u64, _u8p, _int]),
     "pbf_probe": (_int, [_vp, _u8p, _vp, _u64, _u8p, _int]),
     "pbf_probe_multi_fixed": (_int, [_vp, _u32, _u8p, _u32, _u64, _vp, _int]),

@@ -336,6 +336,17 @@ class BloomFilter:
         return f"BloomFilter(nb_bytes={self.nb_bytes}, nb_hash_functions={self.nb_hash_functions}, device={self.device})"
 
 
+def murmur3(key, seed: int = 0, device: Optional[int] = None) -> int:
+    """mmh3.hash(key, seed) — MurmurHash3_x86_32 as the signed int32 bloom_filter.py:46 uses,
+    computed on the device (pbf_murmur3_x86_32).  `key`: str (UTF-8 encoded) or bytes."""
+    enc = key.encode("utf-8") if isinstance(key, str) else bytes(key)
+    out = ctypes.c_int32(0)
+    dev = _default_device if device is None else int(device)
+    _native.check(_native.lib().pbf_murmur3_x86_32(dev, enc, len(enc), seed & 0xFFFFFFFF, ctypes.byref(out)),
+                  "pbf_murmur3_x86_32")
+    return out.value
+
+
 # ---------------------------------------------------------------------- multi-filter probe
 def _native_set(filters):
     """Split `filters` into the ones the native multi-probe takes (a device handle, k > 0) and

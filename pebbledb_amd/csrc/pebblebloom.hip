@@ -1363,6 +1363,13 @@ int hash_impl(pbf_filter_t* f, const uint8_t* keys, const uint64_t* offsets, uin
     return PBF_OK;
 }
 
+// mmh3.hash(key, seed) for one key (the signed int32 bloom_filter.py:46 takes): SURVEY.md §8b's
+// pbf_murmur3_x86_32, computed on the device like every other hash of the library.
+__global__ void k_murmur_one(const uint8_t* key, uint32_t len, uint32_t seed, int32_t* out) {
+    if (threadIdx.x != 0) return;
+    murmur_seeds_loop(key, len, 1, [&](int, uint32_t h) { *out = int32_t(h); }, int(seed));
+}
+
 __global__ void k_popcount(const uint32_t* __restrict__ w, uint64_t n, unsigned long long* out) {
     __shared__ unsigned long long part[4];
     unsigned long long s = 0;
@@ -1579,6 +1586,11 @@ int pbf_add_fixed(pbf_filter_t* f, const uint8_t* keys, uint32_t key_len, uint64
     return add_impl(f, keys, nullptr, key_len, n, on_device);
 }
 
+// SURVEY.md §8b's name for the batch add (BloomFilter.add over n keys, bloom_filter.py:60-65).
+int pbf_build(pbf_filter_t* f, const uint8_t* keys, const uint64_t* offsets, uint64_t n, int keys_on_device) {
+    return pbf_add(f, keys, offsets, n, keys_on_device);
+}
+
 int pbf_add(pbf_filter_t* f, const uint8_t* keys, const uint64_t* offsets, uint64_t n, int on_device) {
     if (!offsets && n > 0) return fail(PBF_ERR_INVALID, "null offsets");
     return add_impl(f, keys ? keys : reinterpret_cast<const uint8_t*>(offsets), offsets, 0, n, on_device);
@@ -1671,6 +1683,24 @@ int pbf_sync(pbf_filter_t* f) {
     int rc = enter(f);
     if (rc) return rc;
     return wait_stream(f);
+}
+
+int pbf_murmur3_x86_32(int device, const uint8_t* key, uint64_t len, uint32_t seed, int32_t* out) {
+    if (!out || (len && !key)) return fail(PBF_ERR_INVALID, "null key or out");
+    if (len > kOneKeyMax) return fail(PBF_ERR_INVALID, "key longer than 4096 bytes");
+    HIP_TRY(hipSetDevice(device));
+    OneKeyStage* st = nullptr;
+    int rc = one_key_stage(device, &st);
+    if (rc) return rc;
+    if (len) std::memcpy(st->host + kOneKeyData, key, len);
+    int32_t* res = reinterpret_cast<int32_t*>(st->host + 8);
+    *reinterpret_cast<volatile int32_t*>(res) = 0;
+    k_murmur_one<<<1, 64, 0, nullptr>>>(st->dev + kOneKeyData, uint32_t(len), seed,
+                                          reinterpret_cast<int32_t*>(st->dev + 8));
+    CHECK_LAUNCH();
+    HIP_TRY(hipStreamSynchronize(nullptr));
+    *out = *reinterpret_cast<volatile int32_t*>(res);
+    return PBF_OK;
 }
 
 int pbf_may_contain(pbf_filter_t* f, const uint8_t* key, uint64_t len, int* out) {

@@ -436,3 +436,24 @@ def test_ring_build_super_tiles(nb, k, n, sb, kps):
                        capture_output=True, text=True, timeout=140,
                        cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
+
+
+def test_murmur3_documented_values_and_goldens():
+    """pbf_murmur3_x86_32 on the device: mmh3's documented values and the
+    reference's own hash of 'key1' with seeds 0..3 (tests/golden)."""
+    from pebbledb_amd.bloom_filter import murmur3
+    assert murmur3("foo") == -156908512 and murmur3("foo", 42) == -1322301282
+    assert [murmur3("key1", s) for s in range(4)] == [-1684602587, 1833321129, 386463789, 201916224]
+    for case in load_golden("mmh3_vectors.json")["cases"][:40]:  # seeds 0..15 per key
+        key = bytes.fromhex(case["key_hex"])
+        assert [murmur3(key, s) for s in (0, 1, 7, 15)] == [case["h"][s] for s in (0, 1, 7, 15)], case["key_hex"]
+
+
+def test_bits_outside_the_bitmap_are_dropped_like_to_bytes():
+    """BloomFilter(nb, k, bits=...) with bits wider than 8*nb or negative: the reference keeps the
+    int and only ever reads its low 8*nb_bytes bits (to_bytes, _is_bit_set) — same bytes here."""
+    bf = BloomFilter(8, 3, bits=(1 << 70) | 0b101)
+    assert bf.to_bytes() == (5).to_bytes(8, "little") + b"\x03"
+    neg = BloomFilter(4, 2, bits=-1)
+    assert neg.to_bytes() == b"\xff\xff\xff\xff\x02"
+    assert neg.may_contain("anything") and neg.may_contain("")
