@@ -668,6 +668,18 @@ void set_gather(PartPlan& pl, uint32_t B, uint32_t row, uint32_t nf = 1) {
             pl.lds_gather = with;
         }
     }
+    // the packed-quad loop's region prefix rq[nb + 1] (ring gather)
+    if (pl.pg.ring) pl.lds_gather = ((pl.lds_gather + 3) & ~size_t(3)) + (size_t((B + S - 1) / S) + 1) * 4 + 8;
+}
+
+// The ring gather walks its regions as one packed list of quads (PBF_GATHER_PACKED=0: region by
+// region, the round-1 loop).
+int gather_packed() {
+    static const int v = [] {
+        const char* e = std::getenv("PBF_GATHER_PACKED");
+        return (e && std::atoi(e) == 0) ? 0 : 1;
+    }();
+    return v;
 }
 
 PartPlan plan_ring(uint32_t B, uint32_t k, uint64_t n, uint32_t rc, double share, uint32_t nf = 1,
@@ -910,7 +922,7 @@ int run_tiled_probe_set(pbf_filter_t* f, pbf_filter_t* const* fs, uint32_t nf, c
             }
             CHECK_LAUNCH();
             gring<<<grid, 512, pl.lds_gather, s>>>(tm, pg, b.n, regions, R, fill, subcnt, neg, alive, outs[0] + hm_off,
-                                                  hw, nf, r_words, neg_words, pl.gtq);
+                                                  hw, nf, r_words, neg_words, pl.gtq, gather_packed());
             CHECK_LAUNCH();
             if (use_hw) {
                 for (uint32_t i = 0; i < nf; ++i) {

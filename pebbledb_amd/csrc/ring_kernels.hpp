@@ -280,7 +280,8 @@ __global__ void __launch_bounds__(512) k_gather_ring(TileMap tm, PartGeom pg, ui
                                                      const uint32_t* __restrict__ pref,
                                                      const uint32_t* __restrict__ neg, const uint32_t* __restrict__ alive,
                                                      uint8_t* __restrict__ hitmask, uint32_t* __restrict__ hw,
-                                                     uint32_t nf, uint64_t r_stride, uint64_t neg_stride, uint32_t tq) {
+                                                     uint32_t nf, uint64_t r_stride, uint64_t neg_stride, uint32_t tq,
+                                                     int packed) {
     extern __shared__ uint32_t smem[];
     if constexpr (NFM == 1) nf = 1;
     const uint32_t B = tm.nbuckets, cap = pg.cap, wpr = cap / 32, nqs = pg.nq + 1;
@@ -326,8 +327,97 @@ __global__ void __launch_bounds__(512) k_gather_ring(TileMap tm, PartGeom pg, ui
         }
     }
     lds_barrier();
+    if (packed) {
+        // The split's regions as ONE list of 4-entry quads: rq[bb] = quads of regions before bb
+        // (exclusive prefix of ceil(fill / 4), fill = the row's last pref).  Every load round
+        // then serves 64 quads per wave instruction, however the fills fall, instead of up to
+        // three rounds per region whose last one has few lanes.
+        uint32_t* rq = reinterpret_cast<uint32_t*>(qtab + ((nb * (tq ? tq : 0) + 3) & ~3u));
+        if (wave == 0) {
+            uint32_t carry = 0;
+            for (uint32_t c0 = 0; c0 < nb; c0 += 64) {
+                const uint32_t bb = c0 + lane;
+                uint32_t v = bb < nb ? (uint32_t(lpref[bb * nqs + nqs - 1]) + 3) >> 2 : 0u;
+#pragma unroll
+                for (int d = 1; d < 64; d <<= 1) {
+                    const uint32_t o = __shfl_up(v, d, 64);
+                    if (lane >= uint32_t(d)) v += o;
+                }
+                if (bb < nb) rq[bb + 1] = carry + v;  // inclusive -> exclusive of bb + 1
+                carry += __shfl(v, 63, 64);
+            }
+            if (lane == 0) rq[0] = 0;
+        }
+        lds_barrier();
+        const uint32_t T = rq[nb];
+        constexpr int UP = 4;
+        for (uint32_t base = wave * 64; base < T; base += nwaves * 64 * UP) {
+            uint4 v[UP];
+            uint32_t rw[NFM][UP], bq[UP], rr[UP];
+#pragma unroll
+            for (int u = 0; u < UP; ++u) {
+                const uint32_t s0 = min(base + uint32_t(u) * nwaves * 64, T - 1);
+                const uint32_t qi = min(s0 + lane, T - 1);
+                // the wave's first quad's region (uniform binary search), then each lane steps
+                // over the few region ends among its wave's 64 quads
+                uint32_t lo = 0, len = nb + 1;
+                while (len > 1) {
+                    const uint32_t half = len >> 1;
+                    if (rq[lo + half] <= s0) lo += half;
+                    len -= half;
+                }
+                while (lo + 1 < nb && rq[lo + 1] <= qi) ++lo;
+                bq[u] = lo;
+                rr[u] = (qi - rq[lo]) * 4;
+                const uint64_t reg = region_id(g, b_lo + lo, pg.G, B);
+                v[u] = ld_stream(regions + reg * cap + rr[u]);
+#pragma unroll
+                for (int f = 0; f < NFM; ++f)
+                    if (uint32_t(f) < nf) rw[f][u] = R[f * r_stride + reg * wpr + (rr[u] >> 5)];
+            }
+#pragma unroll
+            for (int u = 0; u < UP; ++u) {
+                const uint32_t qi = base + uint32_t(u) * nwaves * 64 + lane;
+                if (qi >= T) continue;
+                const uint32_t bb = bq[u], r = rr[u];
+                const uint16_t* pb = lpref + bb * nqs;
+                const uint32_t fillr = pb[nqs - 1];
+                const uint32_t lim = fillr - r < 4 ? (1u << (fillr - r)) - 1u : 0xFu;
+                uint32_t fl[NFM], any = 0;
+#pragma unroll
+                for (int f = 0; f < NFM; ++f) {
+                    fl[f] = uint32_t(f) < nf ? (~r_quad(rw[f][u], r) & lim) : 0u;
+                    any |= fl[f];
+                }
+                if (!any) continue;
+                uint32_t lo = 0;
+                if (tq) {
+                    lo = qtab[bb * tq + (r >> 2)];
+                } else {
+                    uint32_t len = nqs;
+                    while (len > 1) {
+                        const uint32_t half = len >> 1;
+                        if (pb[lo + half] <= r) lo += half;
+                        len -= half;
+                    }
+                }
+                const uint32_t vv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    if ((any >> t) & 1u) {
+                        while (lo + 1 < nqs && pb[lo + 1] <= r + t) ++lo;
+                        const uint32_t jj = lo * 4 + (vv[t] >> 30);
+                        const uint32_t key = jj * kRingKeysPerSub + ((vv[t] >> kSlotShift) & 1023u);
+#pragma unroll
+                        for (int f = 0; f < NFM; ++f)
+                            if ((fl[f] >> t) & 1u) atomicAnd(kbits + f * kw + (key >> 5), ~(1u << (key & 31)));
+                    }
+                }
+            }
+        }
+    }
     constexpr int U = 4;
-    for (uint32_t b0 = b_lo + wave; b0 < b_hi; b0 += nwaves * U) {
+    for (uint32_t b0 = b_lo + wave; !packed && b0 < b_hi; b0 += nwaves * U) {
         uint32_t fillb[U];
 #pragma unroll
         for (int u = 0; u < U; ++u)

@@ -120,6 +120,8 @@ for step in "$@"; do
                 unset PBF_BENCH_DEVICE PBF_BENCH_BACKEND ;;
     gsweepG) for G in ${PBF_GS:-256 512 1024}; do PBF_PART_G=$G run c3_G$G 300 python bench.py --config c3 --steps 3 --warmup 1 --no-cpu-baseline --no-host-inclusive; done
              for G in 256 512; do PBF_PART_G=$G run c2_G$G 300 python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-host-inclusive; done ;;
+    gpacked) for r in 1 2; do for pk in 0 1; do PBF_GATHER_PACKED=$pk run gp${pk}_c2_$r 300 python bench.py --steps 40 --warmup 5 --no-cpu-baseline --no-host-inclusive; done; done
+             for pk in 0 1; do PBF_GATHER_PACKED=$pk run gp${pk}_c5 300 python bench.py --config c5 --steps 5 --warmup 2 --no-cpu-baseline --no-host-c5; done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
