@@ -61,7 +61,7 @@ def test_range_mask_device_resident_and_many_tables():
     enc = [s.encode() for p in bounds for s in p]
     bo = np.zeros(len(enc) + 1, np.uint64)
     np.cumsum([len(e) for e in enc], out=bo[1:])
-    d = {name: torch.from_numpy(a.view(np.int64) if a.dtype == np.uint64 else a).cuda()
+    d = {name: torch.from_numpy((a.view(np.int64) if a.dtype == np.uint64 else a).copy()).cuda()
          for name, a in (("k", pk.data), ("ko", pk.offsets), ("b", np.frombuffer(b"".join(enc), np.uint8).copy()),
                          ("bo", bo))}
     out = torch.zeros(len(bounds) * ((len(keys) + 7) // 8), dtype=torch.uint8, device="cuda")
