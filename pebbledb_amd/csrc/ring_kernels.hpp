@@ -106,6 +106,7 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
         }
     };
     load_batch(k0);
+    PBF_STAMP(7);
     uint32_t j = 0;
     for (uint64_t c0 = k0; c0 < k1; c0 += uint64_t(P) * kps) {
         uint4 cw[F16 ? P : 1];
@@ -115,6 +116,13 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
             if constexpr (F16) cw[u] = kw[u];
             ca[u] = aw[u];
         }
+#ifdef PBF_STAMPS
+        if constexpr (F16) {  // the batch's key-load wait, stamped on its own
+            PBF_STAMP(9);
+            asm volatile("" ::"v"(cw[0].x), "v"(cw[P - 1].w));
+            PBF_STAMP(10);
+        }
+#endif
         if (c0 + uint64_t(P) * kps < k1) load_batch(c0 + uint64_t(P) * kps);
 #pragma unroll
         for (int u = 0; u < P; ++u, ++j) {
@@ -134,6 +142,7 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
 #ifndef PBF_RING_HASH_LATE
             // hash before the barrier: a wave done with its share of the previous flush hashes
             // while the others still flush
+            PBF_STAMP(6);
             if (live) hash();
 #endif
             PBF_STAMP(0);
@@ -222,6 +231,7 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
             PBF_STAMP(5);
         }
     }
+    PBF_STAMP(8);
     lds_barrier();
     // The last partial group of every tile leaves as a whole group too (entries past the fill
     // count are never read; the region has room: head is a multiple of GS and cap of 32).

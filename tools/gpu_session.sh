@@ -76,6 +76,8 @@ for step in "$@"; do
     variants) for v in build/variants/*.so; do nm=$(basename $v .so); PBF_LIB=$PWD/$v run var_$nm 300 python bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-host-inclusive; done
               run var_default 300 python bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-host-inclusive ;;
     variants_c3) for r in 1 2; do for v in build/variants/*.so; do nm=$(basename $v .so); PBF_LIB=$PWD/$v run c3var_${nm}_$r 300 python bench.py --config c3 --steps 5 --warmup 2 --no-cpu-baseline --no-host-inclusive; done; done ;;
+    parity) run parity 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_device_resident.py -m gpu -x -q -rf --timeout 150 --timeout-method thread ;;
+    benchq) for r in 1 2; do run benchq_$r 300 python bench.py --steps 40 --warmup 5 --no-cpu-baseline --no-host-inclusive; done ;;
     rphases)run rphases 300 tools/microbench/ring_phases ;;
     phases) run phases_t0 300 tools/microbench/part_phases 0
             run phases_t16 300 tools/microbench/part_phases 16 ;;

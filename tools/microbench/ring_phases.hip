@@ -1,6 +1,7 @@
 // Diagnostic: per-phase cycle shares of k_part_ring (workgroup 0, wave 0) via s_memtime stamps.
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -DPBF_STAMPS -o ring_phases ring_phases.hip
-// Phases: 0-1 barrier, 1-2 LDS atomics + head reads, 2-3 ring writes, 3-4 barrier, 4-5 flush.
+// Phases: 6-0 hash (incl. the key-load wait), 0-1 barrier, 1-2 LDS atomics + head reads,
+// 2-3 ring writes, 3-4 barrier, 4-5 flush, 5-6 loop / key-load issue.
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
@@ -17,7 +18,7 @@ void run(const char* name, uint8_t* keys, uint64_t n, int k, uint32_t* alive) {
     PartGeom pg{};
     uint64_t kpw = (n + 255) / 256; kpw = (kpw + 1023) / 1024 * 1024;
     pg.G = uint32_t((n + kpw - 1) / kpw); pg.kps = 1024; pg.kpw = kpw; pg.nsub = uint32_t(kpw / 1024);
-    pg.nq = (pg.nsub + 3) / 4; pg.ring = 32; pg.cap = 4096;
+    pg.nq = (pg.nsub + 3) / 4; pg.ring = 32; pg.cap = 4096; pg.sb = 0; pg.nsup = B;
     uint32_t *regions, *fill, *pref, *ovf, *cnt, *neg, *bitmap;
     hipMalloc(&regions, size_t(pg.G) * B * pg.cap * 4); hipMalloc(&fill, size_t(pg.G) * B * 4);
     hipMalloc(&pref, size_t(pg.G) * B * (pg.nq + 1) * 4); hipMalloc(&ovf, n * k * 4); hipMalloc(&cnt, 64);
@@ -43,13 +44,20 @@ void run(const char* name, uint8_t* keys, uint64_t n, int k, uint32_t* alive) {
     float ms; hipEventElapsedTime(&ms, a, b);
     std::vector<unsigned long long> h(64);
     hipMemcpy(h.data(), st, 64 * 8, hipMemcpyDeviceToHost);
-    const char* names[] = {"barrier", "atomics+head", "ring writes", "barrier", "flush"};
-    double tot = 0;
-    for (int p = 0; p < 5; ++p) tot += double(h[p + 1] - h[p]);
-    printf("%s: %.1f us (stamped), G=%u nsub=%u (hash = the rest of the iteration)\n", name, ms * 1e3, pg.G, pg.nsub);
-    for (int p = 0; p < 5; ++p)
-        printf("   %-12s %6.1f%%  %8.0f cycles/sub-chunk\n", names[p], 100.0 * double(h[p + 1] - h[p]) / tot,
-               double(h[p + 1] - h[p]) / pg.nsub);
+    // phases 0-4 within a sub-chunk; 6->0 = hash; key wait = 9->10 (per batch);
+    // rest = total (7->8) minus all of these (loop, load issue, pref)
+    const char* names[] = {"barrier A", "atomics+head", "ring writes", "barrier B", "flush", "hash", "key wait", "rest"};
+    double d[8];
+    for (int p = 0; p < 5; ++p) d[p] = double(h[p + 1] - h[p]);
+    d[5] = double(h[0]) - double(h[6]);
+    d[6] = double(h[10]) - double(h[9]);
+    const double tot = double(h[8]) - double(h[7]);
+    d[7] = tot;
+    for (int p = 0; p < 7; ++p) d[7] -= d[p];
+    printf("%s: %.1f us (stamped), G=%u nsub=%u, wave 0 loop %.0f cycles/sub-chunk\n", name, ms * 1e3, pg.G,
+           pg.nsub, tot / pg.nsub);
+    for (int p = 0; p < 8; ++p)
+        printf("   %-12s %6.1f%%  %8.0f cycles/sub-chunk\n", names[p], 100.0 * d[p] / tot, d[p] / pg.nsub);
     hipFree(regions); hipFree(fill); hipFree(pref); hipFree(ovf); hipFree(cnt); hipFree(neg); hipFree(bitmap); hipFree(st);
 }
 
