@@ -761,14 +761,41 @@ PartPlan plan_for(const TileMap& tm, uint32_t k, int km, uint64_t n, bool probe,
     uint32_t sb, nsup, kps;
     if (!probe && ring_build_geometry(B, k, &sb, &nsup, &kps)) {
         const PartPlan pl = plan_ring(B, k, n, 32, share, 1, sb, kps);
-        if (pl.pg.cap < (1u << 20)) return pl;
+        // flush descriptors hold a region position in 20 bits; entry offsets within a
+        // workgroup's regions are 32-bit (nsup * cap < 2^32)
+        if (pl.pg.cap < (1u << 20) && uint64_t(pl.pg.nsup) * pl.pg.cap < (uint64_t(1) << 32)) return pl;
     }
     const uint32_t rc = probe ? ring_entries(B, k, probe, tm.tb) : 0;
     if (rc) {
         const PartPlan pl = plan_ring(B, k, n, rc, share, nf);
-        if (pl.pg.cap < (1u << 20)) return pl;  // flush descriptors hold a region position in 20 bits
+        if (pl.pg.cap < (1u << 20) && uint64_t(pl.pg.nsup) * pl.pg.cap < (uint64_t(1) << 32)) return pl;
     }
     return plan_partition(B, k, km, n, probe, share);
+}
+
+// The ring partition kernel for (k, key layout, ring size): with the seed count and the 32-entry
+// ring fixed at compile time where it pays (k equal to the register bucket, or k = 6 — C2/C5's
+// k), its k LDS atomics per key issue back to back and its ring / flush arithmetic is shifts;
+// other k or ring sizes take the runtime kernel of their bucket.
+template <int KX, int KMD, bool PROBE, class L>
+void with_ring_kernel(uint32_t k, uint32_t ring, bool pow2, L&& launch) {
+    if constexpr (KMD != kFixedN) {
+        if (ring == 32) {
+            if constexpr (KX == 8) {
+                if (k == 6) {
+                    launch(pow2 ? k_part_ring<6, KMD, PROBE, true, true, 32>
+                                : k_part_ring<6, KMD, PROBE, false, true, 32>);
+                    return;
+                }
+            }
+            if (k == uint32_t(KX)) {
+                launch(pow2 ? k_part_ring<KX, KMD, PROBE, true, true, 32>
+                            : k_part_ring<KX, KMD, PROBE, false, true, 32>);
+                return;
+            }
+        }
+    }
+    launch(pow2 ? k_part_ring<KX, KMD, PROBE, true> : k_part_ring<KX, KMD, PROBE, false>);
 }
 
 int run_tiled(pbf_filter_t* f, const Batch& b) {
@@ -798,11 +825,13 @@ int run_tiled(pbf_filter_t* f, const Batch& b) {
             constexpr int KX = decltype(KMAX)::value, KMD = decltype(KM)::value;
             if (pg.ring) {
                 if constexpr (KX <= 16) {
-                    auto kern = ring_pow2(tm) ? k_part_ring<KX, KMD, false, true> : k_part_ring<KX, KMD, false, false>;
-                    err = allow_lds(kern, pl.lds_part);
-                    if (err == hipSuccess)
-                        kern<<<pg.G, kPartThreads, pl.lds_part, s>>>(b.ks, b.n, int(k), tm, pg, regions, fill, nullptr,
-                                                             ovf, ovf_count, ProbeSet{}, 0, nullptr, nullptr);
+                    with_ring_kernel<KX, KMD, false>(k, pg.ring, ring_pow2(tm), [&](auto kern) {
+                        err = allow_lds(kern, pl.lds_part);
+                        if (err == hipSuccess)
+                            kern<<<pg.G, kPartThreads, pl.lds_part, s>>>(b.ks, b.n, int(k), tm, pg, regions, fill,
+                                                                 nullptr, ovf, ovf_count, ProbeSet{}, 0, nullptr,
+                                                                 nullptr);
+                    });
                 }
             } else {
                 auto kern = k_part<KX, KMD, false>;
@@ -889,12 +918,13 @@ int run_tiled_probe_set(pbf_filter_t* f, pbf_filter_t* const* fs, uint32_t nf, c
                 constexpr int KX = decltype(KMAX)::value, KMD = decltype(KM)::value;
                 if (pg.ring) {
                     if constexpr (KX <= 16) {
-                        auto kern = ring_pow2(tm) ? k_part_ring<KX, KMD, true, true> : k_part_ring<KX, KMD, true, false>;
-                        err = allow_lds(kern, pl.lds_part);
-                        if (err == hipSuccess)
-                            kern<<<pg.G, kPartThreads, pl.lds_part, s>>>(b.ks, b.n, int(kr), tm, pg, regions, fill,
-                                                                 subcnt, nullptr, nullptr, ps, sbase, alive,
-                                                                 use_hw ? hw : nullptr);
+                        with_ring_kernel<KX, KMD, true>(kr, pg.ring, ring_pow2(tm), [&](auto kern) {
+                            err = allow_lds(kern, pl.lds_part);
+                            if (err == hipSuccess)
+                                kern<<<pg.G, kPartThreads, pl.lds_part, s>>>(b.ks, b.n, int(kr), tm, pg, regions,
+                                                                     fill, subcnt, nullptr, nullptr, ps, sbase,
+                                                                     alive, use_hw ? hw : nullptr);
+                        });
                     }
                 } else {
                     auto kern = k_part<KX, KMD, true>;

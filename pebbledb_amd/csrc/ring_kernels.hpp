@@ -51,7 +51,11 @@ __device__ __forceinline__ uint32_t ring_pos(uint32_t h, const TileMap& tm) {
 // Keys are loaded kRingPrefetch sub-chunks at a time, one batch ahead.  On gfx950 vmcnt also
 // counts stores, so the wait for a key load also waits for every flush store issued before it;
 // batching pays that wait once per kRingPrefetch sub-chunks instead of once per sub-chunk.
-template <int KMAX, int KM, bool PROBE, bool POW2>
+// EXACT: k == KMAX is known at compile time, so the per-seed `s < k` tests vanish and the k LDS
+// atomics of a key issue back to back instead of one uniform branch (and one wait) per seed.
+// RCT: the ring size at compile time (0 = pg.ring), so ring addresses, the flush's group count
+// (a division by GS) and its lane split are shifts instead of multiplies and a runtime divide.
+template <int KMAX, int KM, bool PROBE, bool POW2, bool EXACT = false, int RCT = 0>
 __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k, TileMap tm, PartGeom pg,
                                                     uint32_t* __restrict__ regions, uint32_t* __restrict__ fill,
                                                     uint32_t* __restrict__ pref, uint32_t* __restrict__ ovf,
@@ -59,12 +63,13 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
                                                     ProbeSet ps, int sbase, const uint32_t* __restrict__ alive,
                                                     uint32_t* __restrict__ hw_init) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    if constexpr (EXACT) k = KMAX;
     // rings per super-tile of 2^sb tiles (builds of filters with more tiles than the LDS has
     // rings for; probes: sb = 0, nsup = the tile count)
     const uint32_t B = pg.nsup;
     const uint32_t shift = tm.tb + pg.sb;
     const uint32_t kps = pg.kps;  // keys per sub-chunk (<= 1024 threads)
-    const uint32_t RC = pg.ring, GS = RC / 2, rmask = RC - 1;
+    const uint32_t RC = RCT ? uint32_t(RCT) : pg.ring, GS = RC / 2, rmask = RC - 1;
     const uint32_t tid = threadIdx.x, nt = blockDim.x;
     const uint32_t lane = tid & 63, wave = tid >> 6;
     const uint32_t g = blockIdx.x;
@@ -74,6 +79,13 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
     // tile's flush cursor with its slot (no separate head read per position)
     unsigned long long* ht = reinterpret_cast<unsigned long long*>(smem);  // B
     uint32_t* desc = smem + 2 * B;                           // 16 waves x 128 group descriptors
+#ifndef PBF_REGION_TILE_MAJOR
+    // this workgroup's regions; an entry's offset in them fits 32 bits (B * cap < 2^32)
+    uint32_t* const rgn = regions + uint64_t(g) * B * cap;
+    auto region_at = [&](uint32_t tb, uint32_t e) { return rgn + (tb * cap + e); };
+#else
+    auto region_at = [&](uint32_t tb, uint32_t e) { return regions + region_id(g, tb, pg.G, B) * cap + e; };
+#endif
     uint32_t* ring = smem + ((2 * B + 16 * 128 + 3) & ~3u);  // B * RC, 16-B aligned
     const uint32_t nqs = pg.nq + 1;  // pref entries per (g, b)
     for (uint32_t b = tid; b < B; b += nt) {
@@ -102,7 +114,11 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
         for (int u = 0; u < P; ++u) {
             const uint64_t i = c0 + uint64_t(u) * kps + tid;
             aw[u] = (alive && i < k1) ? alive[i >> 5] : ~0u;
+#ifdef PBF_DIAG_SYNTH_KEYS  // diagnostic (tools/microbench): keys made in registers, no key loads
+            if constexpr (F16) kw[u] = make_uint4(uint32_t(i), uint32_t(i) * 0x9E3779B9u, uint32_t(i >> 7) ^ 0x55u, uint32_t(i) + 17u);
+#else
             if constexpr (F16) kw[u] = ld_stream_nt<PBF_NT_KEYS != 0>(reinterpret_cast<const uint32_t*>(ks.data) + min(i, n - 1) * 4);
+#endif
         }
     };
     load_batch(k0);
@@ -218,7 +234,10 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
                         const uint32_t tb = d & 0xFFFu;
                         const uint32_t e = (d >> 12) + q * 4;  // region position
                         const uint4 v = *reinterpret_cast<const uint4*>(ring + tb * RC + (e & rmask));
-                        st_stream<(PBF_NT_STORE & (PROBE ? 2 : 1)) != 0>(regions + region_id(g, tb, pg.G, B) * cap + e, v);
+#ifdef PBF_DIAG_NO_STORES  // diagnostic (tools/microbench): the flush's group stores left out
+                        if (v.x == 0xFFFFFFFFu && v.y == 0xFFFFFFFFu && v.z == 0xFFFFFFFFu && v.w == 0xFFFFFFFFu)
+#endif
+                        st_stream<(PBF_NT_STORE & (PROBE ? 2 : 1)) != 0>(region_at(tb, e), v);
                     }
                 }
                 __builtin_amdgcn_wave_barrier();
@@ -253,7 +272,7 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
                     const uint32_t tb = d & 0xFFFu;
                     const uint32_t e = (d >> 12) + q * 4;
                     const uint4 v = *reinterpret_cast<const uint4*>(ring + tb * RC + (e & rmask));
-                    st_stream<(PBF_NT_STORE & (PROBE ? 2 : 1)) != 0>(regions + region_id(g, tb, pg.G, B) * cap + e, v);
+                    st_stream<(PBF_NT_STORE & (PROBE ? 2 : 1)) != 0>(region_at(tb, e), v);
                 }
             }
             __builtin_amdgcn_wave_barrier();

@@ -79,6 +79,7 @@ for step in "$@"; do
     parity) run parity 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_device_resident.py -m gpu -x -q -rf --timeout 150 --timeout-method thread ;;
     benchq) for r in 1 2; do run benchq_$r 300 python bench.py --steps 40 --warmup 5 --no-cpu-baseline --no-host-inclusive; done ;;
     rphases)run rphases 300 tools/microbench/ring_phases ;;
+    rtime) for b in ring_time ring_time_synth ring_time_nostore ring_time_synth_nostore; do run $b 300 tools/microbench/$b; done ;;
     phases) run phases_t0 300 tools/microbench/part_phases 0
             run phases_t16 300 tools/microbench/part_phases 16 ;;
     gapdiag) run native0 120 tools/microbench/pipeline_bench 50 0

@@ -1,5 +1,6 @@
 // Diagnostic: per-phase cycle shares of k_part_ring (workgroup 0, wave 0) via s_memtime stamps.
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -DPBF_STAMPS -o ring_phases ring_phases.hip
+// (without -DPBF_STAMPS: plain launch times; add -DPBF_DIAG_SYNTH_KEYS for keys made in registers)
 // Phases: 6-0 hash (incl. the key-load wait), 0-1 barrier, 1-2 LDS atomics + head reads,
 // 2-3 ring writes, 3-4 barrier, 4-5 flush, 5-6 loop / key-load issue.
 #include <cstdio>
@@ -7,8 +8,13 @@
 #include <vector>
 #include "../../pebbledb_amd/csrc/ring_kernels.hpp"
 using namespace pbf;
+#ifdef PBF_STAMPS
+constexpr bool kStamped = true;
+#else
+constexpr bool kStamped = false;
+#endif
 
-template <int KMAX, bool PROBE>
+template <int KMAX, bool PROBE, bool EXACT = false>
 void run(const char* name, uint8_t* keys, uint64_t n, int k, uint32_t* alive) {
     const uint64_t nb_bytes = 1ull << 27;
     TileMap tm{};
@@ -25,10 +31,12 @@ void run(const char* name, uint8_t* keys, uint64_t n, int k, uint32_t* alive) {
     hipMalloc(&neg, n / 8 + 64); hipMalloc(&bitmap, nb_bytes);
     hipMemset(cnt, 0, 64); hipMemset(neg, 0, n / 8 + 64); hipMemset(bitmap, 0, nb_bytes);
     unsigned long long* st; hipMalloc(&st, 64 * 8); hipMemset(st, 0, 64 * 8);
+#ifdef PBF_STAMPS
     hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &st, sizeof(st));
+#endif
     KeySet ks{keys, nullptr, nullptr, 16};
     const size_t lds = size_t((2 * B + 16 * 128 + 3) & ~3u) * 4 + size_t(B) * 32 * 4;
-    auto kern = k_part_ring<KMAX, 0, PROBE, true>;
+    auto kern = k_part_ring<KMAX, 0, PROBE, true, EXACT, EXACT ? 32 : 0>;
     ProbeSet ps{};
     ps.nf = PROBE ? 1 : 0;
     ps.bm[0] = bitmap;
@@ -40,8 +48,12 @@ void run(const char* name, uint8_t* keys, uint64_t n, int k, uint32_t* alive) {
     hipMemset(st, 0, 64 * 8);
     hipEventRecord(a);
     kern<<<pg.G, 1024, lds>>>(ks, n, k, tm, pg, regions, fill, pref, ovf, cnt, ps, PROBE ? 1 : 0, alive, nullptr);
+    for (int r = 0; r < 4; ++r)  // unstamped builds: 5 timed launches
+        if (!kStamped) kern<<<pg.G, 1024, lds>>>(ks, n, k, tm, pg, regions, fill, pref, ovf, cnt, ps, PROBE ? 1 : 0, alive, nullptr);
     hipEventRecord(b); hipEventSynchronize(b);
     float ms; hipEventElapsedTime(&ms, a, b);
+    if (!kStamped) printf("%s: %.1f us per launch (unstamped)\n", name, ms * 1e3 / 5);
+    if (kStamped) {
     std::vector<unsigned long long> h(64);
     hipMemcpy(h.data(), st, 64 * 8, hipMemcpyDeviceToHost);
     // phases 0-4 within a sub-chunk; 6->0 = hash; key wait = 9->10 (per batch);
@@ -58,6 +70,7 @@ void run(const char* name, uint8_t* keys, uint64_t n, int k, uint32_t* alive) {
            pg.nsub, tot / pg.nsub);
     for (int p = 0; p < 8; ++p)
         printf("   %-12s %6.1f%%  %8.0f cycles/sub-chunk\n", names[p], 100.0 * d[p] / tot, d[p] / pg.nsub);
+    }
     hipFree(regions); hipFree(fill); hipFree(pref); hipFree(ovf); hipFree(cnt); hipFree(neg); hipFree(bitmap); hipFree(st);
 }
 
@@ -73,5 +86,7 @@ int main() {
     run<4, true>("probe round 1 (k=1), 20M keys", keys, n, 1, nullptr);
     run<8, true>("probe round 2 (k=5, half alive), 20M keys", keys, n, 5, alive);
     run<8, true>("probe k=6 single round, 20M keys", keys, n, 6, nullptr);
+    run<6, false, true>("build k=6 EXACT, 10M keys", keys, n / 2, 6, nullptr);
+    run<6, true, true>("probe k=6 EXACT single round, 20M keys", keys, n, 6, nullptr);
     return 0;
 }
