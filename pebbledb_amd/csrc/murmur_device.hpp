@@ -163,14 +163,16 @@ __device__ __forceinline__ void murmur_seeds_chunked(const uint8_t* p, uint32_t 
 }
 
 // Fixed 16-byte keys from one 16-byte load (the C2/C4/C5 key shape).
+// The first round, rotl(seed ^ m0, 13), is rotl(m0, 13) ^ rotl(seed, 13): the key's part is
+// rotated once for all seeds, the seed's part is uniform (scalar) — one vector op per seed saved.
 template <int KMAX, class Emit>
 __device__ __forceinline__ void murmur_seeds16(uint4 w, int k, Emit&& emit, int sbase = 0) {
     const uint32_t m0 = mix_block(w.x), m1 = mix_block(w.y), m2 = mix_block(w.z), m3 = mix_block(w.w);
+    const uint32_t r0 = rotl32(m0, 13);
 #pragma unroll
     for (int s = 0; s < KMAX; ++s) {
         if (s < k) {
-            uint32_t h = uint32_t(sbase + s);
-            h = round_h(h, m0);
+            uint32_t h = times5(r0 ^ rotl32(uint32_t(sbase + s), 13)) + 0xe6546b64u;
             h = round_h(h, m1);
             h = round_h(h, m2);
             h = round_h(h, m3);

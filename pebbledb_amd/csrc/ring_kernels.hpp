@@ -221,8 +221,11 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
                     ng = (t - h) / GS;
                 }
                 const uint64_t m1 = __ballot(ng >= 1), m2 = __ballot(ng >= 2);
-                const uint64_t below = (uint64_t(1) << lane) - 1;
-                const uint32_t at = __popcll(m1 & below) + __popcll(m2 & below);
+                // descriptors of lower lanes: masked bit counts (v_mbcnt), accumulated over m1, m2
+                const uint32_t at = __builtin_amdgcn_mbcnt_hi(
+                    uint32_t(m2 >> 32), __builtin_amdgcn_mbcnt_lo(
+                                            uint32_t(m2), __builtin_amdgcn_mbcnt_hi(
+                                                              uint32_t(m1 >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m1), 0u))));
                 const uint32_t total = __popcll(m1) + __popcll(m2);
                 if (ng >= 1) wd[at] = b | (h << 12);
                 if (ng >= 2) wd[at + 1] = b | ((h + GS) << 12);
@@ -328,6 +331,18 @@ __global__ void __launch_bounds__(512) k_gather_ring(TileMap tm, PartGeom pg, ui
     uint16_t* lpref = reinterpret_cast<uint16_t*>(kbits + nf * kw);  // nb * nqs (values <= cap < 2^16)
     uint8_t* qtab = reinterpret_cast<uint8_t*>(lpref + ((nb * nqs + 1) & ~1u));  // nb * tq (tq > 0)
     const uint32_t* gp = pref + uint64_t(g) * nqs * B;  // [q][b] in memory, [b][q] in LDS
+#ifndef PBF_REGION_TILE_MAJOR
+    // workgroup g's regions and result words; offsets within them fit 32 bits (B * cap < 2^32)
+    const uint32_t* const rgn = regions + uint64_t(g) * B * cap;
+    const uint32_t* const Rg = R + uint64_t(g) * B * wpr;
+    auto entries_at = [&](uint32_t b, uint32_t r) { return rgn + (b * cap + r); };
+    auto rword = [&](uint32_t f, uint32_t b, uint32_t r) { return Rg[f * r_stride + (b * wpr + (r >> 5))]; };
+#else
+    auto entries_at = [&](uint32_t b, uint32_t r) { return regions + region_id(g, b, pg.G, B) * cap + r; };
+    auto rword = [&](uint32_t f, uint32_t b, uint32_t r) {
+        return R[f * r_stride + region_id(g, b, pg.G, B) * wpr + (r >> 5)];
+    };
+#endif
     for (uint32_t x = tid; x < nb * nqs; x += nt) {
         const uint32_t q = x / nb, bb = x - q * nb;
         lpref[bb * nqs + q] = uint16_t(gp[uint64_t(q) * B + b_lo + bb]);
@@ -398,11 +413,10 @@ __global__ void __launch_bounds__(512) k_gather_ring(TileMap tm, PartGeom pg, ui
                 while (lo + 1 < nb && rq[lo + 1] <= qi) ++lo;
                 bq[u] = lo;
                 rr[u] = (qi - rq[lo]) * 4;
-                const uint64_t reg = region_id(g, b_lo + lo, pg.G, B);
-                v[u] = ld_stream(regions + reg * cap + rr[u]);
+                v[u] = ld_stream(entries_at(b_lo + lo, rr[u]));
 #pragma unroll
                 for (int f = 0; f < NFM; ++f)
-                    if (uint32_t(f) < nf) rw[f][u] = R[f * r_stride + reg * wpr + (rr[u] >> 5)];
+                    if (uint32_t(f) < nf) rw[f][u] = rword(f, b_lo + lo, rr[u]);
             }
 #pragma unroll
             for (int u = 0; u < UP; ++u) {
@@ -461,11 +475,10 @@ __global__ void __launch_bounds__(512) k_gather_ring(TileMap tm, PartGeom pg, ui
             for (int u = 0; u < U; ++u) {
                 const uint32_t b = min(b0 + u * nwaves, b_hi - 1);
                 const uint32_t r = min(r0 + lane * 4, (max(fillb[u], 1u) - 1) & ~3u);
-                const uint64_t reg = region_id(g, b, pg.G, B);
-                v[u] = ld_stream(regions + reg * cap + r);
+                v[u] = ld_stream(entries_at(b, r));
 #pragma unroll
                 for (int f = 0; f < NFM; ++f)
-                    if (uint32_t(f) < nf) rw[f][u] = R[f * r_stride + reg * wpr + (r >> 5)];
+                    if (uint32_t(f) < nf) rw[f][u] = rword(f, b, r);
             }
 #pragma unroll
             for (int u = 0; u < U; ++u) {
