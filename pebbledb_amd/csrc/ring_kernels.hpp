@@ -445,10 +445,17 @@ __global__ void __launch_bounds__(512) k_gather_ring(TileMap tm, PartGeom pg, ui
                     }
                 }
                 const uint32_t vv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+                // the next group's first entry: a boundary inside the quad is rare (a group
+                // holds ~24 entries at C2), so entries usually take lo with one compare
+                uint32_t nxt = lo + 1 < nqs ? uint32_t(pb[lo + 1]) : 0xFFFFFFFFu;
 #pragma unroll
                 for (int t = 0; t < 4; ++t) {
                     if ((any >> t) & 1u) {
-                        while (lo + 1 < nqs && pb[lo + 1] <= r + t) ++lo;
+                        if (r + t >= nxt) {
+                            ++lo;
+                            while (lo + 1 < nqs && pb[lo + 1] <= r + t) ++lo;
+                            nxt = lo + 1 < nqs ? uint32_t(pb[lo + 1]) : 0xFFFFFFFFu;
+                        }
                         const uint32_t jj = lo * 4 + (vv[t] >> 30);
                         const uint32_t key = jj * kRingKeysPerSub + ((vv[t] >> kSlotShift) & 1023u);
 #pragma unroll
@@ -508,10 +515,17 @@ __global__ void __launch_bounds__(512) k_gather_ring(TileMap tm, PartGeom pg, ui
                             }
                         }
                         const uint32_t vv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+                        // the next group's first entry: a boundary inside the quad is rare (a
+                        // group holds ~24 entries at C2), so entries usually take lo with one compare
+                        uint32_t nxt = lo + 1 < nqs ? uint32_t(pb[lo + 1]) : 0xFFFFFFFFu;
 #pragma unroll
                         for (int t = 0; t < 4; ++t) {
                             if ((any >> t) & 1u) {
-                                while (lo + 1 < nqs && pb[lo + 1] <= r + t) ++lo;
+                                if (r + t >= nxt) {
+                                    ++lo;
+                                    while (lo + 1 < nqs && pb[lo + 1] <= r + t) ++lo;
+                                    nxt = lo + 1 < nqs ? uint32_t(pb[lo + 1]) : 0xFFFFFFFFu;
+                                }
                                 const uint32_t jj = lo * 4 + (vv[t] >> 30);
                                 const uint32_t key = jj * kRingKeysPerSub + ((vv[t] >> kSlotShift) & 1023u);
 #pragma unroll

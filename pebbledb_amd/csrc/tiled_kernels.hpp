@@ -500,10 +500,12 @@ __global__ void __launch_bounds__(256) k_ovf_build(TileMap tm, const uint32_t* _
 // (l = the entry's 16-byte piece of the word, t = its place in the piece).  This is the layout
 // four wave ballots produce when 8 lanes read a word piece by piece (k_tile_probe).
 // r_quad: the 4 result bits of the piece holding entries r..r+3 (r % 4 == 0).
+// The four bits sit at l, 8+l, 16+l, 24+l; after the shift and mask, one multiply by 0x01020408
+// moves byte t's bit to bit 24+t (the other partial products land below bit 24 or above bit 31,
+// each on its own bit, so nothing carries into 24..27).
 __device__ __forceinline__ uint32_t r_quad(uint32_t rw, uint32_t r) {
-    const uint32_t l = (r & 31) >> 2;
-    return ((rw >> l) & 1u) | (((rw >> (8 + l)) & 1u) << 1) | (((rw >> (16 + l)) & 1u) << 2) |
-           (((rw >> (24 + l)) & 1u) << 3);
+    const uint32_t x = (rw >> ((r & 31) >> 2)) & 0x01010101u;
+    return (x * 0x01020408u) >> 24;
 }
 
 // One workgroup per tile.  Region words are read 8 per wave instruction: lane = one 16-byte

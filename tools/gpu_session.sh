@@ -77,6 +77,8 @@ for step in "$@"; do
               run var_default 300 python bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-host-inclusive ;;
     variants_c3) for r in 1 2; do for v in build/variants/*.so; do nm=$(basename $v .so); PBF_LIB=$PWD/$v run c3var_${nm}_$r 300 python bench.py --config c3 --steps 5 --warmup 2 --no-cpu-baseline --no-host-inclusive; done; done ;;
     parity) run parity 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_device_resident.py -m gpu -x -q -rf --timeout 150 --timeout-method thread ;;
+    profq) run profq 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/profq -o run -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-host-inclusive
+           python tools/prof_summary.py gpurun_out/profq > gpurun_out/profq_summary.txt 2>&1 || true ;;
     benchq) for r in 1 2; do run benchq_$r 300 python bench.py --steps 40 --warmup 5 --no-cpu-baseline --no-host-inclusive; done ;;
     rphases)run rphases 300 tools/microbench/ring_phases ;;
     rtime) for b in ring_time ring_time_synth ring_time_nostore ring_time_synth_nostore; do run $b 300 tools/microbench/$b; done ;;
