@@ -903,10 +903,15 @@ int run_tiled_probe_set(pbf_filter_t* f, pbf_filter_t* const* fs, uint32_t nf, c
     ps.neg_stride = neg_words;
     for (uint32_t i = 0; i < nf; ++i) ps.bm[i] = fs[i]->bitmap;
     size_t lds_tile = ((size_t(1) << tm.tb) / 32 + 2 * pg.G + 1 + 16) * 4;
-    const size_t lds_expand = size_t(pg.G) * (pg.cap / 32) * 2;
-    const int expand = lds_tile + lds_expand <= 160 * 1024 ? 1 : 0;
+    // the tile test's per-word table: u32 global word index + u8 filled-entry count per word
+    const size_t lds_expand = size_t(pg.G) * (pg.cap / 32) * 5;
+    const bool expand = lds_tile + lds_expand <= 160 * 1024;
     if (expand) lds_tile += lds_expand;
-    HIP_TRY(allow_lds(k_tile_probe, lds_tile));
+    // a region word's global index (region * cap/32 + word) is 32-bit
+    if (uint64_t(pg.G) * B * (pg.cap / 32) >= (uint64_t(1) << 32)) return fail(PBF_ERR_INVALID, "probe scratch too large");
+    auto tprobe = expand ? k_tile_probe<true> : k_tile_probe<false>;
+    auto tprobe_set = expand ? k_tile_probe_set<true> : k_tile_probe_set<false>;
+    HIP_TRY(allow_lds(tprobe, lds_tile));
     // One probe round: seeds [sbase, sbase + kr) of the keys `alive` marks (all if null), each
     // filter's round hit mask (AND alive) into outs[i] + hm_off.
     auto round = [&](int sbase, uint32_t kr, const uint32_t* alive, uint8_t* const* outs) -> int {
@@ -945,11 +950,11 @@ int run_tiled_probe_set(pbf_filter_t* f, pbf_filter_t* const* fs, uint32_t nf, c
             // every filter's tile test (one XCD-aware launch for a set), then ONE gather over
             // the shared region entries
             if (nf == 1) {
-                k_tile_probe<<<B, 1024, lds_tile, s>>>(tm, pg, regions, fill, fs[0]->bitmap, R, expand);
+                tprobe<<<B, 1024, lds_tile, s>>>(tm, pg, regions, fill, fs[0]->bitmap, R);
             } else {
-                HIP_TRY(allow_lds(k_tile_probe_set, lds_tile));
+                HIP_TRY(allow_lds(tprobe_set, lds_tile));
                 const uint32_t grid = ((B + 7) / 8) * 8 * nf;
-                k_tile_probe_set<<<grid, 1024, lds_tile, s>>>(tm, pg, regions, fill, ps, R, r_words, expand);
+                tprobe_set<<<grid, 1024, lds_tile, s>>>(tm, pg, regions, fill, ps, R, r_words);
             }
             CHECK_LAUNCH();
             gring<<<grid, 512, pl.lds_gather, s>>>(tm, pg, b.n, regions, R, fill, subcnt, neg, alive, outs[0] + hm_off,
@@ -966,7 +971,7 @@ int run_tiled_probe_set(pbf_filter_t* f, pbf_filter_t* const* fs, uint32_t nf, c
         }
         for (uint32_t i = 0; i < nf; ++i) {
             if (S > 1) HIP_TRY(hipMemsetAsync(hw, 0xFF, neg_bytes, s));
-            k_tile_probe<<<B, 1024, lds_tile, s>>>(tm, pg, regions, fill, fs[i]->bitmap, R, expand);
+            tprobe<<<B, 1024, lds_tile, s>>>(tm, pg, regions, fill, fs[i]->bitmap, R);
             CHECK_LAUNCH();
             k_gather<<<grid, 512, pl.lds_gather, s>>>(tm, pg, b.n, regions, R, subcnt, neg + i * neg_words,
                                                       outs[i] + hm_off, hw);

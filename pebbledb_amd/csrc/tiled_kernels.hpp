@@ -511,20 +511,24 @@ __device__ __forceinline__ uint32_t r_quad(uint32_t rw, uint32_t r) {
 // One workgroup per tile.  Region words are read 8 per wave instruction: lane = one 16-byte
 // piece of a word, so an instruction reads 1 KiB contiguously (words are consecutive within a
 // region).  Each lane tests its 4 entries in the LDS tile; four ballots give every word's 32
-// result bits, stored by the word's first lane.  `expand` = the LDS budget allows a per-word
-// region id table (else a binary search over the word prefix).
-template <bool NT>
+// result bits, stored by the word's first lane.
+// EXPAND (the LDS budget allows it): a per-word table gives word c's global index
+// wo = region * (cap / 32) + word-in-region — the region word's address / 32 AND its result
+// word's index — and its count of filled entries, so a load needs one LDS read and the wave's
+// U loads issue back to back.  Otherwise the word's region comes from a binary search over the
+// word prefix.
+template <bool NT, bool EXPAND>
 __device__ __forceinline__ void tile_probe_body(uint32_t* smem, uint32_t b, const TileMap& tm, const PartGeom& pg,
                                                 const uint32_t* __restrict__ regions, const uint32_t* __restrict__ fill,
-                                                const uint32_t* __restrict__ bitmap, uint32_t* __restrict__ R,
-                                                int expand) {
+                                                const uint32_t* __restrict__ bitmap, uint32_t* __restrict__ R) {
     const uint32_t B = tm.nbuckets, G = pg.G, cap = pg.cap, wpr = cap / 32;
     const uint32_t W = 1u << (tm.tb - 5);
     uint32_t* tile = smem;          // W
     uint32_t* fills = tile + W;     // G
     uint32_t* wpre = fills + G;     // G+1
     uint32_t* ws = wpre + G + 1;    // 16
-    uint16_t* wq = reinterpret_cast<uint16_t*>(ws + 16);  // G*wpr (expand)
+    uint32_t* wo = ws + 16;                                     // G*wpr (EXPAND)
+    uint8_t* wn = reinterpret_cast<uint8_t*>(wo + G * wpr);     // G*wpr (EXPAND)
     const uint64_t w0 = tile_word0(b, tm);
     const uint32_t nw = uint32_t(min<uint64_t>(W, tm.total_words - w0));
     const uint32_t tid = threadIdx.x, nt = blockDim.x;
@@ -533,9 +537,16 @@ __device__ __forceinline__ void tile_probe_body(uint32_t* smem, uint32_t b, cons
     lds_barrier();
     block_exclusive_scan(fills, wpre, G, ws);
     for (uint32_t q = tid; q < G; q += nt) {
-        fills[q] = fill[uint64_t(b) * G + q];  // entries again
-        if (expand)
-            for (uint32_t c = wpre[q]; c < wpre[q + 1]; ++c) wq[c] = uint16_t(q);
+        const uint32_t fq = fill[uint64_t(b) * G + q];
+        fills[q] = fq;  // entries again
+        if constexpr (EXPAND) {
+            const uint32_t base = uint32_t(region_id(q, b, G, B)) * wpr;
+            for (uint32_t c = wpre[q]; c < wpre[q + 1]; ++c) {
+                const uint32_t word = c - wpre[q];
+                wo[c] = base + word;
+                wn[c] = uint8_t(min(fq - word * 32, 32u));
+            }
+        }
     }
     lds_barrier();
     const uint32_t lmask = (1u << tm.tb) - 1u;
@@ -546,44 +557,50 @@ __device__ __forceinline__ void tile_probe_body(uint32_t* smem, uint32_t b, cons
     constexpr int U = 8;  // instructions (8 words each) in flight per wave
     for (uint32_t c0 = wave * 8; c0 < total; c0 += stride * U) {
         uint4 v[U];
-        uint32_t qq[U], word[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint32_t c = min(c0 + u * stride + wsub, total - 1);  // unconditional loads
-            qq[u] = expand ? uint32_t(wq[c]) : bucket_of(wpre, G, c);
-            word[u] = c - wpre[qq[u]];
-            v[u] = ld_stream_nt<NT>(regions + region_id(qq[u], b, G, B) * cap + word[u] * 32 + l * 4);
-        }
+        uint32_t oo[U], lim[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint32_t c = c0 + u * stride + wsub;
-            const uint32_t e = word[u] * 32 + l * 4;
-            const uint32_t lim = c < total ? fills[qq[u]] : 0u;  // entries past the fill read as 0
+            const uint32_t cc = min(c, total - 1);  // unconditional loads
+            if constexpr (EXPAND) {
+                oo[u] = wo[cc];
+                lim[u] = c < total ? uint32_t(wn[cc]) : 0u;  // entries past the fill read as 0
+            } else {
+                const uint32_t qq = bucket_of(wpre, G, cc);
+                const uint32_t word = cc - wpre[qq];
+                oo[u] = uint32_t(region_id(qq, b, G, B)) * wpr + word;
+                lim[u] = c < total ? min(fills[qq] - word * 32, 32u) : 0u;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = ld_stream_nt<NT>(regions + uint64_t(oo[u]) * 32 + l * 4);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t e = l * 4;
             uint32_t p = v[u].x & lmask;
-            const bool t0 = (e < lim) & bool((tile[p >> 5] >> (p & 31)) & 1u);
+            const bool t0 = (e < lim[u]) & bool((tile[p >> 5] >> (p & 31)) & 1u);
             p = v[u].y & lmask;
-            const bool t1 = (e + 1 < lim) & bool((tile[p >> 5] >> (p & 31)) & 1u);
+            const bool t1 = (e + 1 < lim[u]) & bool((tile[p >> 5] >> (p & 31)) & 1u);
             p = v[u].z & lmask;
-            const bool t2 = (e + 2 < lim) & bool((tile[p >> 5] >> (p & 31)) & 1u);
+            const bool t2 = (e + 2 < lim[u]) & bool((tile[p >> 5] >> (p & 31)) & 1u);
             p = v[u].w & lmask;
-            const bool t3 = (e + 3 < lim) & bool((tile[p >> 5] >> (p & 31)) & 1u);
+            const bool t3 = (e + 3 < lim[u]) & bool((tile[p >> 5] >> (p & 31)) & 1u);
             const uint64_t m0 = __ballot(t0), m1 = __ballot(t1), m2 = __ballot(t2), m3 = __ballot(t3);
-            if (l == 0 && c < total) {
+            if (l == 0 && c0 + u * stride + wsub < total) {
                 const uint32_t sh = wsub * 8;
-                R[region_id(qq[u], b, G, B) * wpr + word[u]] =
-                    uint32_t((m0 >> sh) & 0xFF) | (uint32_t((m1 >> sh) & 0xFF) << 8) |
-                    (uint32_t((m2 >> sh) & 0xFF) << 16) | (uint32_t((m3 >> sh) & 0xFF) << 24);
+                R[oo[u]] = uint32_t((m0 >> sh) & 0xFF) | (uint32_t((m1 >> sh) & 0xFF) << 8) |
+                           (uint32_t((m2 >> sh) & 0xFF) << 16) | (uint32_t((m3 >> sh) & 0xFF) << 24);
             }
         }
     }
 }
 
+template <bool EXPAND>
 __global__ void __launch_bounds__(1024) k_tile_probe(TileMap tm, PartGeom pg, const uint32_t* __restrict__ regions,
                                                      const uint32_t* __restrict__ fill,
-                                                     const uint32_t* __restrict__ bitmap, uint32_t* __restrict__ R,
-                                                     int expand) {
+                                                     const uint32_t* __restrict__ bitmap, uint32_t* __restrict__ R) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-    tile_probe_body<PBF_NT_LOAD != 0>(smem, blockIdx.x, tm, pg, regions, fill, bitmap, R, expand);
+    tile_probe_body<PBF_NT_LOAD != 0, EXPAND>(smem, blockIdx.x, tm, pg, regions, fill, bitmap, R);
 }
 
 // The tile test of a multi-filter probe in ONE launch: workgroup (tile b, filter f) for every
@@ -591,9 +608,10 @@ __global__ void __launch_bounds__(1024) k_tile_probe(TileMap tm, PartGeom pg, co
 // only, never correctness), so block x = ((b / 8) * nf + f) * 8 + b % 8 puts the nf
 // workgroups of tile b on one XCD, dispatched together: they stream the same region entries
 // (g, b), g = 0..G-1, in the same order, and all but the first read them from that XCD's L2.
+template <bool EXPAND>
 __global__ void __launch_bounds__(1024) k_tile_probe_set(TileMap tm, PartGeom pg, const uint32_t* __restrict__ regions,
                                                          const uint32_t* __restrict__ fill, ProbeSet ps,
-                                                         uint32_t* __restrict__ R, uint64_t r_stride, int expand) {
+                                                         uint32_t* __restrict__ R, uint64_t r_stride) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     const uint32_t x = blockIdx.x, nf = ps.nf;
     const uint32_t t = x >> 3;
@@ -601,7 +619,7 @@ __global__ void __launch_bounds__(1024) k_tile_probe_set(TileMap tm, PartGeom pg
     const uint32_t b = (t / nf) * 8 + (x & 7);
     if (b >= tm.nbuckets) return;
     // the set's other workgroups of tile b read the same lines: temporal loads keep them in L2
-    tile_probe_body<false>(smem, b, tm, pg, regions, fill, ps.bm[f], R + f * r_stride, expand);
+    tile_probe_body<false, EXPAND>(smem, b, tm, pg, regions, fill, ps.bm[f], R + f * r_stride);
 }
 
 // Workgroup g owns keys [g*kpw, (g+1)*kpw) and regions (g, 0..B-1).  It reads each region once,

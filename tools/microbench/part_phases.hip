@@ -47,10 +47,10 @@ int main(int argc, char** argv) {
             uint32_t* R; uint8_t* hm;
             hipMalloc(&R, size_t(pg.G) * B * (pg.cap / 32) * 4); hipMalloc(&hm, n / 8 + 64);
             const size_t lt = (size_t(1) << 20) / 8 + (2 * pg.G + 17) * 4;
-            hipFuncSetAttribute((const void*)k_tile_probe, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lt);
+            hipFuncSetAttribute((const void*)k_tile_probe<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lt);
             hipEvent_t c, d; hipEventCreate(&c); hipEventCreate(&d);
             hipEventRecord(c);
-            k_tile_probe<<<B, 1024, lt>>>(tm, pg, regions, fill, bitmap, R, 0);
+            k_tile_probe<false><<<B, 1024, lt>>>(tm, pg, regions, fill, bitmap, R);
             hipEventRecord(d); hipEventSynchronize(d); hipEventElapsedTime(&ms_tile, c, d);
             const size_t lg = size_t((pg.kpw + 31) / 32) * 4 + size_t(B) * (pg.nsub + 1) * 2 + 16;
             hipFuncSetAttribute((const void*)k_gather, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lg);
