@@ -798,6 +798,22 @@ void with_ring_kernel(uint32_t k, uint32_t ring, bool pow2, L&& launch) {
     launch(pow2 ? k_part_ring<KX, KMD, PROBE, true> : k_part_ring<KX, KMD, PROBE, false>);
 }
 
+// The counting-sort partition kernel for (k, key layout): exact-k variants for the k the
+// configurations use (6: C2/C5 shapes, 8: C3, 10: the fp = 0.001 product sizing of C4 / SSTables).
+template <int KX, int KMD, bool PROBE, class L>
+void with_part_kernel(uint32_t k, L&& launch) {
+    if constexpr (KMD != kFixedN) {
+        if constexpr (KX == 8) {
+            if (k == 6) return launch(k_part<6, KMD, PROBE, true>);
+            if (k == 8) return launch(k_part<8, KMD, PROBE, true>);
+        }
+        if constexpr (KX == 16) {
+            if (k == 10) return launch(k_part<10, KMD, PROBE, true>);
+        }
+    }
+    launch(k_part<KX, KMD, PROBE>);
+}
+
 int run_tiled(pbf_filter_t* f, const Batch& b) {
     const TileMap& tm = f->tm;
     const uint32_t B = tm.nbuckets;
@@ -834,11 +850,12 @@ int run_tiled(pbf_filter_t* f, const Batch& b) {
                     });
                 }
             } else {
-                auto kern = k_part<KX, KMD, false>;
-                err = allow_lds(kern, pl.lds_part);
-                if (err == hipSuccess)
-                    kern<<<pg.G, kPartThreads, pl.lds_part, s>>>(b.ks, b.n, int(k), tm, pg, regions, fill, nullptr, ovf,
-                                                         ovf_count, ProbeSet{});
+                with_part_kernel<KX, KMD, false>(k, [&](auto kern) {
+                    err = allow_lds(kern, pl.lds_part);
+                    if (err == hipSuccess)
+                        kern<<<pg.G, kPartThreads, pl.lds_part, s>>>(b.ks, b.n, int(k), tm, pg, regions, fill, nullptr,
+                                                             ovf, ovf_count, ProbeSet{});
+                });
             }
         }
     });
@@ -932,11 +949,12 @@ int run_tiled_probe_set(pbf_filter_t* f, pbf_filter_t* const* fs, uint32_t nf, c
                         });
                     }
                 } else {
-                    auto kern = k_part<KX, KMD, true>;
-                    err = allow_lds(kern, pl.lds_part);
-                    if (err == hipSuccess)
-                        kern<<<pg.G, kPartThreads, pl.lds_part, s>>>(b.ks, b.n, int(kr), tm, pg, regions, fill, subcnt,
-                                                             nullptr, nullptr, ps);
+                    with_part_kernel<KX, KMD, true>(kr, [&](auto kern) {
+                        err = allow_lds(kern, pl.lds_part);
+                        if (err == hipSuccess)
+                            kern<<<pg.G, kPartThreads, pl.lds_part, s>>>(b.ks, b.n, int(kr), tm, pg, regions, fill,
+                                                                 subcnt, nullptr, nullptr, ps);
+                    });
                 }
             }
         });

@@ -238,7 +238,8 @@ __host__ __device__ constexpr int part_kpt(int kmax, int km, bool probe) {
     return kmax <= 4 ? 4 : (kmax <= 8 ? 2 : 1);
 }
 
-template <int KMAX, int KM, bool PROBE>
+// EXACT: k == KMAX at compile time (no per-seed branches; the seeds' LDS atomics issue together).
+template <int KMAX, int KM, bool PROBE, bool EXACT = false>
 __global__ void __launch_bounds__(kPartThreads) k_part(KeySet ks, uint64_t n, int k, TileMap tm, PartGeom pg,
                                                        uint32_t* __restrict__ regions, uint32_t* __restrict__ fill,
                                                        uint32_t* __restrict__ subcnt, uint32_t* __restrict__ ovf,
@@ -246,6 +247,7 @@ __global__ void __launch_bounds__(kPartThreads) k_part(KeySet ks, uint64_t n, in
                                                        ProbeSet ps) {
     constexpr int KPT = part_kpt(KMAX, KM, PROBE);
     extern __shared__ uint32_t smem[];
+    if constexpr (EXACT) k = KMAX;
     const uint32_t B = tm.nbuckets;
     const uint32_t tid = threadIdx.x, nt = blockDim.x;
     const uint32_t kpt = pg.kps / nt;  // <= KPT
