@@ -576,18 +576,20 @@ __device__ __forceinline__ void tile_probe_body(uint32_t* smem, uint32_t b, cons
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) v[u] = ld_stream_nt<NT>(regions + uint64_t(oo[u]) * 32 + l * 4);
+        // an entry's tile word: one bit-field extract of bits [5, tb); its bit: one more (the
+        // hardware takes the offset's low 5 bits, so no mask)
+        const uint32_t wbits = tm.tb - 5;
+        auto bit = [&](uint32_t x) { return __builtin_amdgcn_ubfe(tile[__builtin_amdgcn_ubfe(x, 5u, wbits)], x, 1u); };
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint32_t e = l * 4;
-            uint32_t p = v[u].x & lmask;
-            const bool t0 = (e < lim[u]) & bool((tile[p >> 5] >> (p & 31)) & 1u);
-            p = v[u].y & lmask;
-            const bool t1 = (e + 1 < lim[u]) & bool((tile[p >> 5] >> (p & 31)) & 1u);
-            p = v[u].z & lmask;
-            const bool t2 = (e + 2 < lim[u]) & bool((tile[p >> 5] >> (p & 31)) & 1u);
-            p = v[u].w & lmask;
-            const bool t3 = (e + 3 < lim[u]) & bool((tile[p >> 5] >> (p & 31)) & 1u);
-            const uint64_t m0 = __ballot(t0), m1 = __ballot(t1), m2 = __ballot(t2), m3 = __ballot(t3);
+            // one ballot per compare, ANDed as lane masks (a ballot of a combined condition goes
+            // through a VGPR select and a second compare)
+            auto bal = [](bool c) { return __builtin_amdgcn_ballot_w64(c); };
+            const uint64_t m0 = bal(bit(v[u].x) != 0u) & bal(e < lim[u]);
+            const uint64_t m1 = bal(bit(v[u].y) != 0u) & bal(e + 1 < lim[u]);
+            const uint64_t m2 = bal(bit(v[u].z) != 0u) & bal(e + 2 < lim[u]);
+            const uint64_t m3 = bal(bit(v[u].w) != 0u) & bal(e + 3 < lim[u]);
             if (l == 0 && c0 + u * stride + wsub < total) {
                 const uint32_t sh = wsub * 8;
                 R[oo[u]] = uint32_t((m0 >> sh) & 0xFF) | (uint32_t((m1 >> sh) & 0xFF) << 8) |
