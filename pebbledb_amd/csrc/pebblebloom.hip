@@ -778,9 +778,9 @@ PartPlan plan_for(const TileMap& tm, uint32_t k, int km, uint64_t n, bool probe,
 // k), its k LDS atomics per key issue back to back and its ring / flush arithmetic is shifts;
 // other k or ring sizes take the runtime kernel of their bucket.
 template <int KX, int KMD, bool PROBE, class L>
-void with_ring_kernel(uint32_t k, uint32_t ring, bool pow2, L&& launch) {
+void with_ring_kernel(uint32_t k, uint32_t ring, uint32_t cap, bool pow2, L&& launch) {
     if constexpr (KMD != kFixedN) {
-        if (ring == 32) {
+        if (ring == 32 && cap <= 32768) {  // these kernels keep head / tail in 16 bits
             if constexpr (KX == 8) {
                 if (k == 6) {
                     launch(pow2 ? k_part_ring<6, KMD, PROBE, true, true, 32>
@@ -841,7 +841,7 @@ int run_tiled(pbf_filter_t* f, const Batch& b) {
             constexpr int KX = decltype(KMAX)::value, KMD = decltype(KM)::value;
             if (pg.ring) {
                 if constexpr (KX <= 16) {
-                    with_ring_kernel<KX, KMD, false>(k, pg.ring, ring_pow2(tm), [&](auto kern) {
+                    with_ring_kernel<KX, KMD, false>(k, pg.ring, pg.cap, ring_pow2(tm), [&](auto kern) {
                         err = allow_lds(kern, pl.lds_part);
                         if (err == hipSuccess)
                             kern<<<pg.G, kPartThreads, pl.lds_part, s>>>(b.ks, b.n, int(k), tm, pg, regions, fill,
@@ -940,7 +940,7 @@ int run_tiled_probe_set(pbf_filter_t* f, pbf_filter_t* const* fs, uint32_t nf, c
                 constexpr int KX = decltype(KMAX)::value, KMD = decltype(KM)::value;
                 if (pg.ring) {
                     if constexpr (KX <= 16) {
-                        with_ring_kernel<KX, KMD, true>(kr, pg.ring, ring_pow2(tm), [&](auto kern) {
+                        with_ring_kernel<KX, KMD, true>(kr, pg.ring, pg.cap, ring_pow2(tm), [&](auto kern) {
                             err = allow_lds(kern, pl.lds_part);
                             if (err == hipSuccess)
                                 kern<<<pg.G, kPartThreads, pl.lds_part, s>>>(b.ks, b.n, int(kr), tm, pg, regions,

@@ -78,6 +78,29 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
     // ht[b] = head << 32 | tail: one 64-bit LDS atomic add appends a position and returns the
     // tile's flush cursor with its slot (no separate head read per position)
     unsigned long long* ht = reinterpret_cast<unsigned long long*>(smem);  // B
+    // H32 (the compile-time-ring kernels; the host keeps cap <= 32768 for them): head and tail
+    // as the 16-bit halves of one u32, so the append is a 32-bit atomic spread over all 64 LDS
+    // banks instead of a 64-bit one over 32 bank pairs.  A tail never passes cap + one
+    // sub-chunk's appends (the flush clamps it every sub-chunk), so it stays below 2^16.
+    constexpr bool H32 = RCT != 0;
+    uint32_t* const ht32 = smem;
+    auto ht_get = [&](uint32_t b, uint32_t& h, uint32_t& t) {
+        if constexpr (H32) {
+            const uint32_t v = ht32[b];
+            h = v >> 16;
+            t = v & 0xFFFFu;
+        } else {
+            const unsigned long long v = ht[b];
+            h = uint32_t(v >> 32);
+            t = uint32_t(v);
+        }
+    };
+    auto ht_set = [&](uint32_t b, uint32_t h, uint32_t t) {
+        if constexpr (H32)
+            ht32[b] = (h << 16) | t;
+        else
+            ht[b] = (uint64_t(h) << 32) | t;
+    };
     uint32_t* desc = smem + 2 * B;                           // 16 waves x 128 group descriptors
 #ifndef PBF_REGION_TILE_MAJOR
     // this workgroup's regions; an entry's offset in them fits 32 bits (B * cap < 2^32)
@@ -89,7 +112,7 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
     uint32_t* ring = smem + ((2 * B + 16 * 128 + 3) & ~3u);  // B * RC, 16-B aligned
     const uint32_t nqs = pg.nq + 1;  // pref entries per (g, b)
     for (uint32_t b = tid; b < B; b += nt) {
-        ht[b] = 0;
+        ht_set(b, 0, 0);
         if constexpr (PROBE) pref[uint64_t(g) * nqs * B + b] = 0;
     }
     const uint64_t k0 = uint64_t(g) * pg.kpw;
@@ -171,9 +194,15 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
 #pragma unroll
                 for (int s = 0; s < KMAX; ++s) {
                     if (s < k) {
-                        const unsigned long long v = atomicAdd(ht + (pos[s] >> shift), 1ull);
-                        slot[s] = uint32_t(v);
-                        hd[s] = uint32_t(v >> 32);
+                        if constexpr (H32) {
+                            const uint32_t v = atomicAdd(ht32 + (pos[s] >> shift), 1u);
+                            slot[s] = v & 0xFFFFu;
+                            hd[s] = v >> 16;
+                        } else {
+                            const unsigned long long v = atomicAdd(ht + (pos[s] >> shift), 1ull);
+                            slot[s] = uint32_t(v);
+                            hd[s] = uint32_t(v >> 32);
+                        }
                     }
                 }
                 PBF_STAMP(2);
@@ -215,9 +244,9 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
                 const uint32_t b = b0 + lane;
                 uint32_t ng = 0, h = 0, t = 0;
                 if (b < B) {
-                    const unsigned long long hv = ht[b];
-                    h = uint32_t(hv >> 32);
-                    t = min(uint32_t(hv), min(h + RC, cap));  // positions past these left the stream
+                    uint32_t tail;
+                    ht_get(b, h, tail);
+                    t = min(tail, min(h + RC, cap));  // positions past these left the stream
                     ng = (t - h) / GS;
                 }
                 const uint64_t m1 = __ballot(ng >= 1), m2 = __ballot(ng >= 2);
@@ -245,7 +274,7 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
                 }
                 __builtin_amdgcn_wave_barrier();
                 if (b < B) {
-                    ht[b] = (uint64_t(h + ng * GS) << 32) | t;
+                    ht_set(b, h + ng * GS, t);
                     if constexpr (PROBE)
                         if (((j + 1) & 3) == 0) pref[(uint64_t(g) * nqs + ((j + 1) >> 2)) * B + b] = t;
                 }
@@ -262,11 +291,12 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
         const uint32_t lpg = GS / 4, gpi = 64 / lpg;
         for (uint32_t b0 = wave * 64; b0 < B; b0 += nt) {
             const uint32_t b = b0 + lane;
-            const unsigned long long hv = b < B ? ht[b] : 0ull;
-            const bool part = uint32_t(hv) > uint32_t(hv >> 32);
+            uint32_t hh = 0, tt = 0;
+            if (b < B) ht_get(b, hh, tt);
+            const bool part = tt > hh;
             const uint64_t m1 = __ballot(part);
             const uint32_t at = __popcll(m1 & ((uint64_t(1) << lane) - 1)), total = __popcll(m1);
-            if (part) wd[at] = b | (uint32_t(hv >> 32) << 12);
+            if (part) wd[at] = b | (hh << 12);
             __builtin_amdgcn_wave_barrier();
             for (uint32_t c = 0; c < total; c += gpi) {
                 const uint32_t gi = c + lane / lpg, q = lane % lpg;
@@ -283,7 +313,8 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
     }
     // fill counts; the probe's remaining cumulative counts
     for (uint32_t b = tid; b < B; b += nt) {
-        const uint32_t t = uint32_t(ht[b]);
+        uint32_t hh, t;
+        ht_get(b, hh, t);
         fill[uint64_t(b) * pg.G + g] = t;
         if constexpr (PROBE)
             for (uint32_t q = (j + 3) >> 2; q <= pg.nq; ++q) pref[(uint64_t(g) * nqs + q) * B + b] = t;

@@ -551,7 +551,6 @@ __device__ __forceinline__ void tile_probe_body(uint32_t* smem, uint32_t b, cons
         }
     }
     lds_barrier();
-    const uint32_t lmask = (1u << tm.tb) - 1u;
     const uint32_t total = wpre[G];
     const uint32_t lane = tid & 63, wave = tid >> 6, nwaves = nt >> 6;
     const uint32_t l = lane & 7, wsub = lane >> 3;  // piece of the word, word of the instruction
