@@ -14,7 +14,7 @@ constexpr bool kStamped = true;
 constexpr bool kStamped = false;
 #endif
 
-template <int KMAX, bool PROBE, bool EXACT = false>
+template <int KMAX, bool PROBE, bool EXACT = false, int RCT = 32, int THREADS = 1024>
 void run(const char* name, uint8_t* keys, uint64_t n, int k, uint32_t* alive) {
     const uint64_t nb_bytes = 1ull << 27;
     TileMap tm{};
@@ -22,9 +22,10 @@ void run(const char* name, uint8_t* keys, uint64_t n, int k, uint32_t* alive) {
     tm.tb = 20; tm.nbuckets = 1024; tm.total_words = nb_bytes / 4;
     const uint32_t B = 1024;
     PartGeom pg{};
-    uint64_t kpw = (n + 255) / 256; kpw = (kpw + 1023) / 1024 * 1024;
-    pg.G = uint32_t((n + kpw - 1) / kpw); pg.kps = 1024; pg.kpw = kpw; pg.nsub = uint32_t(kpw / 1024);
-    pg.nq = (pg.nsub + 3) / 4; pg.ring = 32; pg.cap = 4096; pg.sb = 0; pg.nsup = B;
+    const uint64_t groups = 256 * (1024 / THREADS);
+    uint64_t kpw = (n + groups - 1) / groups; kpw = (kpw + THREADS - 1) / THREADS * THREADS;
+    pg.G = uint32_t((n + kpw - 1) / kpw); pg.kps = THREADS; pg.kpw = kpw; pg.nsub = uint32_t(kpw / THREADS);
+    pg.nq = (pg.nsub + 3) / 4; pg.ring = RCT; pg.cap = 4096; pg.sb = 0; pg.nsup = B;
     uint32_t *regions, *fill, *pref, *ovf, *cnt, *neg, *bitmap;
     hipMalloc(&regions, size_t(pg.G) * B * pg.cap * 4); hipMalloc(&fill, size_t(pg.G) * B * 4);
     hipMalloc(&pref, size_t(pg.G) * B * (pg.nq + 1) * 4); hipMalloc(&ovf, n * k * 4); hipMalloc(&cnt, 64);
@@ -35,8 +36,8 @@ void run(const char* name, uint8_t* keys, uint64_t n, int k, uint32_t* alive) {
     hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &st, sizeof(st));
 #endif
     KeySet ks{keys, nullptr, nullptr, 16};
-    const size_t lds = size_t((2 * B + 16 * 128 + 3) & ~3u) * 4 + size_t(B) * 32 * 4;
-    auto kern = k_part_ring<KMAX, 0, PROBE, true, EXACT, EXACT ? 32 : 0>;
+    const size_t lds = size_t((2 * B + 16 * 128 + 3) & ~3u) * 4 + size_t(B) * RCT * 4;
+    auto kern = k_part_ring<KMAX, 0, PROBE, true, EXACT, EXACT ? RCT : 0>;
     ProbeSet ps{};
     ps.nf = PROBE ? 1 : 0;
     ps.bm[0] = bitmap;
@@ -44,12 +45,12 @@ void run(const char* name, uint8_t* keys, uint64_t n, int k, uint32_t* alive) {
     ps.neg_stride = n / 32 + 1;
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipEvent_t a, b; hipEventCreate(&a); hipEventCreate(&b);
-    kern<<<pg.G, 1024, lds>>>(ks, n, k, tm, pg, regions, fill, pref, ovf, cnt, ps, PROBE ? 1 : 0, alive, nullptr);
+    kern<<<pg.G, THREADS, lds>>>(ks, n, k, tm, pg, regions, fill, pref, ovf, cnt, ps, PROBE ? 1 : 0, alive, nullptr);
     hipMemset(st, 0, 64 * 8);
     hipEventRecord(a);
-    kern<<<pg.G, 1024, lds>>>(ks, n, k, tm, pg, regions, fill, pref, ovf, cnt, ps, PROBE ? 1 : 0, alive, nullptr);
+    kern<<<pg.G, THREADS, lds>>>(ks, n, k, tm, pg, regions, fill, pref, ovf, cnt, ps, PROBE ? 1 : 0, alive, nullptr);
     for (int r = 0; r < 4; ++r)  // unstamped builds: 5 timed launches
-        if (!kStamped) kern<<<pg.G, 1024, lds>>>(ks, n, k, tm, pg, regions, fill, pref, ovf, cnt, ps, PROBE ? 1 : 0, alive, nullptr);
+        if (!kStamped) kern<<<pg.G, THREADS, lds>>>(ks, n, k, tm, pg, regions, fill, pref, ovf, cnt, ps, PROBE ? 1 : 0, alive, nullptr);
     hipEventRecord(b); hipEventSynchronize(b);
     float ms; hipEventElapsedTime(&ms, a, b);
     if (!kStamped) printf("%s: %.1f us per launch (unstamped)\n", name, ms * 1e3 / 5);
@@ -88,5 +89,7 @@ int main() {
     run<8, true>("probe k=6 single round, 20M keys", keys, n, 6, nullptr);
     run<6, false, true>("build k=6 EXACT, 10M keys", keys, n / 2, 6, nullptr);
     run<6, true, true>("probe k=6 EXACT single round, 20M keys", keys, n, 6, nullptr);
+    run<6, false, true, 16, 512>("build k=6 EXACT ring 16, 512 threads (2 per CU), 10M keys", keys, n / 2, 6, nullptr);
+    run<6, true, true, 16, 512>("probe k=6 EXACT ring 16, 512 threads (2 per CU), 20M keys", keys, n, 6, nullptr);
     return 0;
 }

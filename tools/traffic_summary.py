@@ -47,7 +47,7 @@ def pass_of(kernel: str) -> str | None:
         # k_part<KMAX, KM, PROBE> / k_part_ring<KMAX, KM, PROBE, POW2>
         args = kernel[kernel.index("<") + 1:].rstrip(">").split(",")
         return "probe" if args[2].strip() == "true" else "build"
-    if kernel in ("pbf::k_tile_build", "pbf::k_ovf_build"):
+    if kernel.split("<")[0] in ("pbf::k_tile_build", "pbf::k_ovf_build"):
         return "build"
     # templated kernels (k_gather_ring<NF>) match on the name before the argument list
     if kernel.split("<")[0] in ("pbf::k_tile_probe", "pbf::k_gather", "pbf::k_gather_ring", "pbf::k_hw_to_hitmask"):
