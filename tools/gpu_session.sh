@@ -76,6 +76,19 @@ for step in "$@"; do
     variants) for v in build/variants/*.so; do nm=$(basename $v .so); PBF_LIB=$PWD/$v run var_$nm 300 python bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-host-inclusive; done
               run var_default 300 python bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-host-inclusive ;;
     variants_c3) for r in 1 2; do for v in build/variants/*.so; do nm=$(basename $v .so); PBF_LIB=$PWD/$v run c3var_${nm}_$r 300 python bench.py --config c3 --steps 5 --warmup 2 --no-cpu-baseline --no-host-inclusive; done; done ;;
+    final2) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+            run pytest 900 python -u -m pytest tests -m gpu -x -v -rf --timeout 150 --timeout-method thread
+            run bench 600 python bench.py
+            run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-host-inclusive
+            python tools/prof_summary.py gpurun_out/prof > gpurun_out/prof_summary.txt 2>&1 || true
+            run pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_fetch -o run -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-host-inclusive
+            run pmc_write 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_write -o run -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-host-inclusive
+            python tools/traffic_summary.py gpurun_out/pmc_fetch gpurun_out/pmc_write gpurun_out/traffic_c2.json > gpurun_out/traffic_summary.txt 2>&1 || true ;;
+    others) run bench_c1 300 python bench.py --config c1 --steps 50 --warmup 5
+            run bench_c3 600 python bench.py --config c3 --steps 5 --warmup 2
+            run bench_c4 600 python bench.py --config c4 --steps 3 --warmup 1
+            run bench_c5 600 python bench.py --config c5 --steps 5 --warmup 2
+            run bench_sst 600 python bench.py --config sst --steps 20 --warmup 3 ;;
     parity) run parity 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_device_resident.py -m gpu -x -q -rf --timeout 150 --timeout-method thread ;;
     profq) run profq 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/profq -o run -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-host-inclusive
            python tools/prof_summary.py gpurun_out/profq > gpurun_out/profq_summary.txt 2>&1 || true ;;
