@@ -46,8 +46,8 @@ SEED_VAR = 0xC3
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS) + ["c4", "c5", "sst"])
     ap.add_argument("--c4-keys", type=int, default=125_000_000, help="c4: keys per filter (reference 125M)")
     ap.add_argument("--c5-probes", type=int, default=100_000_000, help="c5: probe keys (reference 100M)")
