@@ -65,8 +65,9 @@ def build_ingest(force: bool = False, verbose: bool = True) -> str:
     out = ingest_path()
     if not force and os.path.exists(out) and os.path.getmtime(out) >= os.path.getmtime(INGEST_SRC):
         return out
-    cmd = [os.environ.get("CC", "gcc"), "-O2", "-fPIC", "-shared", "-Wall", "-Wextra", "-Wno-missing-field-initializers",
-           "-Wno-unused-parameter", "-I", sysconfig.get_paths()["include"], "-o", out + ".tmp", INGEST_SRC]
+    cmd = [os.environ.get("CC", "gcc"), "-O2", "-fPIC", "-shared", "-fopenmp", "-Wall", "-Wextra",
+           "-Wno-missing-field-initializers", "-Wno-unused-parameter", "-I", sysconfig.get_paths()["include"],
+           "-o", out + ".tmp", INGEST_SRC]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)

@@ -256,9 +256,175 @@ fail:
  * second, both clipped to the data as Python slicing clips them.  A key that is not valid UTF-8
  * raises UnicodeDecodeError and a size field cut short raises struct.error, as the reference's
  * decoder would; a negative size raises ValueError (the reference would slice backwards). */
+/* Strict UTF-8 check, the rules of CPython's decoder (what key.decode("utf-8") accepts): no
+ * continuation or 0xC0/0xC1/0xF5+ lead bytes, no overlong 3- and 4-byte forms, no surrogates
+ * (ED A0..BF), nothing above U+10FFFF (F4 90+), no truncated sequence. */
+static int utf8_valid(const unsigned char* s, size_t n) {
+    size_t i = 0;
+    while (i < n) {
+        const unsigned c = s[i];
+        if (c < 0x80) {
+            ++i;
+            continue;
+        }
+        size_t len;
+        unsigned lo = 0x80, hi = 0xBF;  // range of the first continuation byte
+        if (c >= 0xC2 && c <= 0xDF) {
+            len = 2;
+        } else if (c >= 0xE0 && c <= 0xEF) {
+            len = 3;
+            if (c == 0xE0) lo = 0xA0;
+            if (c == 0xED) hi = 0x9F;
+        } else if (c >= 0xF0 && c <= 0xF4) {
+            len = 4;
+            if (c == 0xF0) lo = 0x90;
+            if (c == 0xF4) hi = 0x8F;
+        } else {
+            return 0;
+        }
+        if (i + len > n) return 0;
+        if (s[i + 1] < lo || s[i + 1] > hi) return 0;
+        for (size_t j = 2; j < len; ++j)
+            if ((s[i + j] & 0xC0) != 0x80) return 0;
+        i += len;
+    }
+    return 1;
+}
+
+/* The parallel form of pack_encoded for a list / tuple of exact bytes objects (the memtable's
+ * records as they come out of memtable.map.values()).  Pass 1 (threads) splits every record
+ * and validates non-ASCII keys; a prefix sum places them; pass 2 (threads) copies keys and
+ * values to their final offsets.  The calling thread keeps the GIL throughout, so no Python
+ * code can change the list or free a record while the worker threads (plain memory reads, no
+ * Python API) look at them; touching the million scattered objects in parallel is the point.
+ * Returns Py_None (no exception) when an item is not an exact bytes object or a record is
+ * malformed: the serial loop below then runs from the start and raises exactly what the
+ * reference's decoder would, in its order. */
+typedef struct {
+    const unsigned char* d;   // the record's bytes
+    uint32_t kl, vo, vl, ok;  // clipped key length (key at d + 4), value start and length
+} RecSplit;
+
+static PyObject* pack_encoded_parallel(PyObject* seq) {
+    const Py_ssize_t n = PySequence_Fast_GET_SIZE(seq);
+    PyObject** items = PySequence_Fast_ITEMS(seq);
+    RecSplit* rs = (RecSplit*)malloc(sizeof(*rs) * (size_t)(n ? n : 1));
+    if (!rs) return PyErr_NoMemory();
+    int bad = 0, ascii = 1;
+    uint64_t min_len = UINT64_MAX, max_len = 0, kt = 0, vt = 0;
+#pragma omp parallel for schedule(static) reduction(| : bad) reduction(& : ascii) reduction(min : min_len) \
+    reduction(max : max_len)
+    for (Py_ssize_t i = 0; i < n; ++i) {
+        PyObject* o = items[i];
+        rs[i].ok = 0;
+        if (Py_TYPE(o) != &PyBytes_Type) {
+            bad = 1;
+            continue;
+        }
+        const unsigned char* r = (const unsigned char*)PyBytes_AS_STRING(o);
+        const size_t len = (size_t)PyBytes_GET_SIZE(o);
+        int32_t ks, vs;
+        if (len < 4) {
+            bad = 1;
+            continue;
+        }
+        memcpy(&ks, r, 4);
+        const size_t key_end = 4 + (size_t)(uint32_t)ks;
+        if (ks < 0 || key_end + 4 > len) {
+            bad = 1;
+            continue;
+        }
+        const size_t kl = (size_t)ks;
+        int a = 1;
+        for (size_t c = 0; c < kl; ++c)
+            if (r[4 + c] & 0x80) {
+                a = 0;
+                break;
+            }
+        if (!a) {
+            ascii = 0;
+            if (!utf8_valid(r + 4, kl)) {
+                bad = 1;
+                continue;
+            }
+        }
+        memcpy(&vs, r + key_end, 4);
+        if (vs < 0) {
+            bad = 1;
+            continue;
+        }
+        const size_t v0 = key_end + 4;
+        rs[i].d = r;
+        rs[i].kl = (uint32_t)kl;
+        rs[i].vo = (uint32_t)v0;
+        rs[i].vl = (uint32_t)(v0 + (size_t)vs <= len ? (size_t)vs : len - v0);
+        rs[i].ok = 1;
+        if ((uint64_t)kl < min_len) min_len = (uint64_t)kl;
+        if ((uint64_t)kl > max_len) max_len = (uint64_t)kl;
+    }
+    Buf kb = {0}, ko = {0}, vb = {0}, vo = {0};
+    PyObject* ret = NULL;
+    if (bad) {  // let the serial loop raise the reference's exception
+        Py_INCREF(Py_None);
+        ret = Py_None;
+        goto done;
+    }
+    if (buf_grow(&ko, ((size_t)n + 1) * 8) || buf_grow(&vo, ((size_t)n + 1) * 8)) goto done;
+    {
+        uint64_t* kof = (uint64_t*)ko.p;
+        uint64_t* vof = (uint64_t*)vo.p;
+        kof[0] = vof[0] = 0;
+        for (Py_ssize_t i = 0; i < n; ++i) {
+            kt += rs[i].kl;
+            vt += rs[i].vl;
+            kof[i + 1] = kt;
+            vof[i + 1] = vt;
+        }
+        ko.n = vo.n = ((size_t)n + 1) * 8;
+        if (buf_grow(&kb, kt ? kt : 1) || buf_grow(&vb, vt ? vt : 1)) goto done;
+        kb.n = kt;
+        vb.n = vt;
+        char* kp = kb.p;
+        char* vp = vb.p;
+#pragma omp parallel for schedule(static)
+        for (Py_ssize_t i = 0; i < n; ++i) {
+            memcpy(kp + kof[i], rs[i].d + 4, rs[i].kl);
+            memcpy(vp + vof[i], rs[i].d + rs[i].vo, rs[i].vl);
+        }
+    }
+    if (n == 0) min_len = 0;
+    {
+        PyObject* a = buf_release(&kb);
+        PyObject* b = buf_release(&ko);
+        PyObject* c = buf_release(&vb);
+        PyObject* e = buf_release(&vo);
+        if (a && b && c && e)
+            ret = Py_BuildValue("(NNNNKiKK)", a, b, c, e, (unsigned long long)n, ascii, (unsigned long long)min_len,
+                                (unsigned long long)max_len);
+        else {
+            Py_XDECREF(a);
+            Py_XDECREF(b);
+            Py_XDECREF(c);
+            Py_XDECREF(e);
+        }
+    }
+done:
+    buf_free(&kb);
+    buf_free(&ko);
+    buf_free(&vb);
+    buf_free(&vo);
+    free(rs);
+    return ret;
+}
+
 static PyObject* py_pack_encoded(PyObject* self, PyObject* args) {
     PyObject* iterable;
     if (!PyArg_ParseTuple(args, "O", &iterable)) return NULL;
+    if ((PyList_CheckExact(iterable) || PyTuple_CheckExact(iterable)) && PySequence_Fast_GET_SIZE(iterable) > 4096) {
+        PyObject* r = pack_encoded_parallel(iterable);
+        if (r != Py_None) return r;  // packed, or an exception (out of memory)
+        Py_DECREF(r);
+    }
     PyObject* seq = (PyList_CheckExact(iterable) || PyTuple_CheckExact(iterable)) ? iterable : NULL;
     PyObject* it = seq ? NULL : PyObject_GetIter(iterable);
     if (!seq && !it) return NULL;

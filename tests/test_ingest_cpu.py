@@ -115,3 +115,66 @@ def test_buffers_outlive_the_packer_and_are_writable():
     gc.collect()
     assert data.flags.writeable and data[:8].tobytes() == b"00000000"
     assert data[-8:].tobytes() == b"00099999"
+
+
+def _enc_bytes(kb: bytes, value: bytes) -> bytes:
+    """A record whose key_size is its byte length (what a byte-level writer would store)."""
+    return struct.pack("i", len(kb)) + kb + struct.pack("i", len(value)) + value
+
+
+def _outcome(fn):
+    try:
+        pr = fn()
+    except Exception as e:  # noqa: BLE001 - the exception type is what is compared
+        return type(e)
+    return (pr.keys.data.tobytes(), None if pr.keys.offsets is None else pr.keys.offsets.tobytes(),
+            pr.values.tobytes(), pr.value_offsets.tobytes(), pr.ascii)
+
+
+TRICKY_UTF8 = [b"\xc2\x80", b"\xdf\xbf", b"\xe0\xa0\x80", b"\xed\x9f\xbf", b"\xef\xbf\xbf", b"\xf0\x90\x80\x80",
+               b"\xf4\x8f\xbf\xbf", b"\xc0\x80", b"\xc1\xbf", b"\xe0\x80\x80", b"\xe0\x9f\xbf", b"\xed\xa0\x80",
+               b"\xed\xbf\xbf", b"\xf0\x80\x80\x80", b"\xf0\x8f\xbf\xbf", b"\xf4\x90\x80\x80", b"\xf5\x80\x80\x80",
+               b"\xff", b"\x80", b"\xe2\x82", b"\xf0\x90\x80", b"a\xc3", "ключ🔑".encode(), b"\xe2\x82\xac\x80"]
+
+
+@pytest.mark.parametrize("bad", TRICKY_UTF8)
+def test_parallel_encoded_packer_matches_serial(bad):
+    """Lists of more than 4096 exact bytes records take the threaded packer (csrc/ingest.c
+    pack_encoded_parallel); an iterator takes the serial loop.  Both must give the same buffers,
+    or the same exception, for keys on every edge of CPython's strict UTF-8 decoder."""
+    rng = np.random.default_rng(len(bad))
+    recs = [_enc_bytes(f"k{i:06d}".encode(), rng.integers(0, 256, int(rng.integers(0, 40)),
+                                                           dtype=np.uint8).tobytes()) for i in range(6000)]
+    recs[4321] = _enc_bytes(b"pre" + bad + b"post", b"value")
+    try:
+        (b"pre" + bad + b"post").decode("utf-8")
+        valid = True
+    except UnicodeDecodeError:
+        valid = False
+    par = _outcome(lambda: PackedRecords.from_encoded(recs))
+    ser = _outcome(lambda: PackedRecords.from_encoded(iter(recs)))
+    assert par == ser
+    assert (par is UnicodeDecodeError) == (not valid)
+
+
+def test_parallel_encoded_packer_errors_and_mixed_items():
+    recs = [_enc_bytes(f"key{i:05d}".encode(), b"v" * (i % 7)) for i in range(9000)]
+    base = _outcome(lambda: PackedRecords.from_encoded(iter(recs)))
+    assert _outcome(lambda: PackedRecords.from_encoded(recs)) == base
+    assert _outcome(lambda: PackedRecords.from_encoded(tuple(recs))) == base
+    mixed = list(recs)
+    mixed[10] = bytearray(mixed[10])  # not exact bytes: the serial loop packs the whole list
+    assert _outcome(lambda: PackedRecords.from_encoded(mixed)) == base
+    for i, broken, err in ((8000, b"\x01\x00", struct.error), (5000, struct.pack("i", -1) + b"abcd", ValueError),
+                           (7000, struct.pack("i", 2) + b"ab" + struct.pack("i", -5), ValueError)):
+        r = list(recs)
+        r[i] = broken
+        assert _outcome(lambda: PackedRecords.from_encoded(r)) is err
+        assert _outcome(lambda: PackedRecords.from_encoded(iter(r))) is err
+    # the first bad record decides the exception, as in the reference's in-order decode
+    r = list(recs)
+    r[6000] = b"\x01\x00"
+    r[6500] = _enc_bytes(b"\xff", b"")
+    assert _outcome(lambda: PackedRecords.from_encoded(r)) is struct.error
+    r[5000] = _enc_bytes(b"\xff", b"")
+    assert _outcome(lambda: PackedRecords.from_encoded(r)) is UnicodeDecodeError
