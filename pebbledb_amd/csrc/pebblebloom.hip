@@ -440,9 +440,11 @@ void bitmap_cache_trim(int device) {
     }
 }
 
-// Streams are per device, created once and dealt round-robin to filters (PBF_STREAMS, default
-// 8): creating a HIP stream per filter cost milliseconds per SSTable (measured 8-14 ms of a
-// 1M-record flush), and filters sharing a stream only order their work.
+// Streams are per device, dealt round-robin to filters (PBF_STREAMS, default 8), so filters
+// built or probed together (C4's eight) run on distinct streams, while filters sharing a
+// stream only order their work.  Creating a HIP stream costs 3-15 ms
+// (profiles/r02/s9/create_in_flush.txt): the whole set is created at a device's first filter
+// (which also pays the runtime's start-up), not one per early SSTable.
 hipError_t pooled_stream(int device, hipStream_t* out) {
     static std::mutex mu;
     static std::map<int, std::pair<std::vector<hipStream_t>, size_t>> pools;
@@ -453,13 +455,15 @@ hipError_t pooled_stream(int device, hipStream_t* out) {
     }();
     std::lock_guard<std::mutex> lock(mu);
     auto& pool = pools[device];
-    if (pool.first.size() < nstreams) {
+    while (pool.first.size() < nstreams) {
         hipStream_t st = nullptr;
         const hipError_t e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
-        if (e != hipSuccess) return e;
+        if (e != hipSuccess) {
+            if (pool.first.empty()) return e;
+            (void)hipGetLastError();  // fewer streams than asked for: share the ones there are
+            break;
+        }
         pool.first.push_back(st);
-        *out = st;
-        return hipSuccess;
     }
     *out = pool.first[pool.second++ % pool.first.size()];
     return hipSuccess;
