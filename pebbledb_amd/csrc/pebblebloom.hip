@@ -712,12 +712,19 @@ PartPlan plan_ring(uint32_t B, uint32_t k, uint64_t n, uint32_t rc, double share
     return pl;
 }
 
+// The KMAX of the counting-sort kernel with_part_kernel launches for (k, key layout): the
+// exact-k variants (6, 8, 10) or the register bucket.
+int part_kmax(uint32_t k, int km) {
+    if (km != kFixedN && (k == 6 || k == 8 || k == 10)) return int(k);
+    return kmax_for(k);
+}
+
 PartPlan plan_partition(uint32_t B, uint32_t k, int km, uint64_t n, bool probe, double share) {
     PartPlan pl{};
     const size_t per_entry = probe ? 6 : 4;  // stage u32 (+ u16 tile id for probes)
     const size_t fixed = size_t(3 * B + 1 + 16) * 4;
     // keys per thread per sub-chunk: as many as the registers (part_kpt) and the LDS allow
-    uint64_t kpt = uint64_t(part_kpt(kmax_for(k), km, probe));
+    uint64_t kpt = uint64_t(part_kpt(part_kmax(k, km), km, probe));
     while (kpt > 1 && fixed + kpt * kPartThreads * k * per_entry > 156 * 1024) --kpt;
     if (probe) kpt = std::min<uint64_t>(kpt, (kSlotMask + 1) / kPartThreads);
     const uint64_t kps = kpt * kPartThreads;

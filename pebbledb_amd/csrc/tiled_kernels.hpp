@@ -233,6 +233,7 @@ __host__ __device__ constexpr int part_kpt(int kmax, int km, bool probe) {
     if (km == kFixed16) {
         if (kmax <= 4) return 4;
         if (kmax <= 8) return 3;
+        if (kmax <= 10 && !probe) return 3;  // the exact k = 10 build (C4's product sizing)
         return kmax <= 16 ? 2 : 1;
     }
     return kmax <= 4 ? 4 : (kmax <= 8 ? 2 : 1);
