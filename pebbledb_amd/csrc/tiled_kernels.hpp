@@ -236,6 +236,7 @@ __host__ __device__ constexpr int part_kpt(int kmax, int km, bool probe) {
         if (kmax <= 10 && !probe) return 3;  // the exact k = 10 build (C4's product sizing)
         return kmax <= 16 ? 2 : 1;
     }
+    if (kmax > 4 && kmax <= 8 && !probe) return 3;  // variable-length builds (C3): 3 keys per thread at k = 8
     return kmax <= 4 ? 4 : (kmax <= 8 ? 2 : 1);
 }
 
