@@ -21,7 +21,7 @@ int main(int argc, char** argv) {
         PartGeom pg{};
         uint64_t kpw = (n + 255) / 256; kpw = (kpw + kps - 1) / kps * kps;
         pg.G = uint32_t((n + kpw - 1) / kpw); pg.kps = kps; pg.kpw = kpw; pg.nsub = uint32_t(kpw / kps);
-        pg.cap = 1024; pg.tdepth = T;
+        pg.cap = 1024; pg.nsup = B;
         uint32_t *regions, *fill, *subcnt, *ovf, *cnt, *neg, *bitmap;
         hipMalloc(&regions, size_t(pg.G) * B * pg.cap * 4); hipMalloc(&fill, size_t(pg.G) * B * 4);
         hipMalloc(&subcnt, size_t(pg.G) * pg.nsub * B * 4); hipMalloc(&ovf, n * k * 4); hipMalloc(&cnt, 64);
@@ -30,15 +30,16 @@ int main(int argc, char** argv) {
         unsigned long long* st; hipMalloc(&st, 64 * 8); hipMemset(st, 0, 64 * 8);
         hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &st, sizeof(st));
         KeySet ks{keys, nullptr, nullptr, 16};
-        const size_t lds = size_t((3 * B + 17 + 3) & ~3u) * 4 + size_t(B) * T * 4 + size_t(kps) * k * (probe ? 6 : 4);
+        const size_t lds = size_t(3 * B + 17) * 4 + size_t(kps) * k * (probe ? 6 : 4);
         hipEvent_t a, b; hipEventCreate(&a); hipEventCreate(&b);
         hipEventRecord(a);
         if (probe) {
             hipFuncSetAttribute((const void*)k_part<8, 0, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-            k_part<8, 0, true><<<pg.G, 1024, lds>>>(ks, n, k, tm, pg, regions, fill, subcnt, ovf, cnt, bitmap, neg);
+            ProbeSet ps{}; ps.nf = 1; ps.bm[0] = bitmap; ps.neg = neg; ps.neg_stride = n / 32 + 1;
+            k_part<8, 0, true><<<pg.G, 1024, lds>>>(ks, n, k, tm, pg, regions, fill, subcnt, ovf, cnt, ps);
         } else {
             hipFuncSetAttribute((const void*)k_part<8, 0, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-            k_part<8, 0, false><<<pg.G, 1024, lds>>>(ks, n, k, tm, pg, regions, fill, subcnt, ovf, cnt, bitmap, neg);
+            k_part<8, 0, false><<<pg.G, 1024, lds>>>(ks, n, k, tm, pg, regions, fill, subcnt, ovf, cnt, ProbeSet{});
         }
         hipEventRecord(b); hipEventSynchronize(b);
         float ms; hipEventElapsedTime(&ms, a, b);
@@ -55,7 +56,7 @@ int main(int argc, char** argv) {
             const size_t lg = size_t((pg.kpw + 31) / 32) * 4 + size_t(B) * (pg.nsub + 1) * 2 + 16;
             hipFuncSetAttribute((const void*)k_gather, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lg);
             hipEventRecord(c);
-            k_gather<<<pg.G, 1024, lg>>>(tm, pg, n, regions, R, subcnt, neg, hm);
+            k_gather<<<dim3(pg.G, 1), 512, lg>>>(tm, pg, n, regions, R, subcnt, neg, hm, nullptr);
             hipEventRecord(d); hipEventSynchronize(d); hipEventElapsedTime(&ms_gather, c, d);
             printf("k_tile_probe %.1f us, k_gather %.1f us (stamped)\n", ms_tile * 1e3, ms_gather * 1e3);
         }
