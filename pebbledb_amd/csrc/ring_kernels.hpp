@@ -35,6 +35,7 @@
 namespace pbf {
 
 constexpr uint32_t kRingKeysPerSub = 1024;  // = threads; slot field is 10 bits
+static_assert(kSlotShift == 20 && kRingKeysPerSub == 1024, "ring entry = (j & 3) << 30 | slot << 20 | position");
 // 2 measured best with the non-temporal streams (C2 A/B over 1/2/3/4/8: profiles/r01/s11/ab.txt)
 #ifndef PBF_RING_PREFETCH
 #define PBF_RING_PREFETCH 2
@@ -487,8 +488,8 @@ __global__ void __launch_bounds__(512) k_gather_ring(TileMap tm, PartGeom pg, ui
                             while (lo + 1 < nqs && pb[lo + 1] <= r + t) ++lo;
                             nxt = lo + 1 < nqs ? uint32_t(pb[lo + 1]) : 0xFFFFFFFFu;
                         }
-                        const uint32_t jj = lo * 4 + (vv[t] >> 30);
-                        const uint32_t key = jj * kRingKeysPerSub + ((vv[t] >> kSlotShift) & 1023u);
+                        // key = (4 lo + (j & 3)) * 1024 + slot = lo << 12 | the entry's top 12 bits
+                        const uint32_t key = (lo << 12) + (vv[t] >> kSlotShift);
 #pragma unroll
                         for (int f = 0; f < NFM; ++f)
                             if ((fl[f] >> t) & 1u) atomicAnd(kbits + f * kw + (key >> 5), ~(1u << (key & 31)));
@@ -509,14 +510,42 @@ __global__ void __launch_bounds__(512) k_gather_ring(TileMap tm, PartGeom pg, ui
         for (uint32_t r0 = 0; r0 < maxf; r0 += 256) {
             uint4 v[U];
             uint32_t rw[NFM][U];
+            // single filter: result words first; a quad's entries (only their key ids are
+            // needed) are loaded only when one of its entries failed, so quads that passed (a
+            // probe batch's members) cost their result bits alone.  Multi-filter sets: nearly
+            // every quad fails some filter, so entries and result words go out together.
+            if constexpr (PBF_GATHER_RFIRST && NFM == 1) {
+                uint32_t anyq[U];
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const uint32_t b = min(b0 + u * nwaves, b_hi - 1);
-                const uint32_t r = min(r0 + lane * 4, (max(fillb[u], 1u) - 1) & ~3u);
-                v[u] = ld_stream(entries_at(b, r));
+                for (int u = 0; u < U; ++u) {
+                    const uint32_t b = min(b0 + u * nwaves, b_hi - 1);
+                    const uint32_t r = min(r0 + lane * 4, (max(fillb[u], 1u) - 1) & ~3u);
+                    rw[0][u] = rword(0, b, r);
+                }
 #pragma unroll
-                for (int f = 0; f < NFM; ++f)
-                    if (uint32_t(f) < nf) rw[f][u] = rword(f, b, r);
+                for (int u = 0; u < U; ++u) {
+                    const uint32_t b = b0 + u * nwaves;
+                    const uint32_t r = r0 + lane * 4;
+                    uint32_t a = 0;
+                    if (b < b_hi && r < fillb[u]) {
+                        const uint32_t lim = fillb[u] - r < 4 ? (1u << (fillb[u] - r)) - 1u : 0xFu;
+                        a = ~r_quad(rw[0][u], r) & lim;
+                    }
+                    anyq[u] = a;
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+                    if (anyq[u]) v[u] = ld_stream(entries_at(b0 + u * nwaves, r0 + lane * 4));
+            } else {
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const uint32_t b = min(b0 + u * nwaves, b_hi - 1);
+                    const uint32_t r = min(r0 + lane * 4, (max(fillb[u], 1u) - 1) & ~3u);
+                    v[u] = ld_stream(entries_at(b, r));
+#pragma unroll
+                    for (int f = 0; f < NFM; ++f)
+                        if (uint32_t(f) < nf) rw[f][u] = rword(f, b, r);
+                }
             }
 #pragma unroll
             for (int u = 0; u < U; ++u) {
@@ -549,19 +578,37 @@ __global__ void __launch_bounds__(512) k_gather_ring(TileMap tm, PartGeom pg, ui
                         // the next group's first entry: a boundary inside the quad is rare (a
                         // group holds ~24 entries at C2), so entries usually take lo with one compare
                         uint32_t nxt = lo + 1 < nqs ? uint32_t(pb[lo + 1]) : 0xFFFFFFFFu;
+                        if constexpr (NFM == 1 && PBF_GATHER_BRANCHFREE) {
+                            // one filter: every entry of a failed quad issues its AND, a passed
+                            // entry's with an all-ones mask (most failed quads fail whole: their
+                            // keys are non-members), so the quad takes no per-entry branches
 #pragma unroll
-                        for (int t = 0; t < 4; ++t) {
-                            if ((any >> t) & 1u) {
+                            for (int t = 0; t < 4; ++t) {
                                 if (r + t >= nxt) {
                                     ++lo;
                                     while (lo + 1 < nqs && pb[lo + 1] <= r + t) ++lo;
                                     nxt = lo + 1 < nqs ? uint32_t(pb[lo + 1]) : 0xFFFFFFFFu;
                                 }
-                                const uint32_t jj = lo * 4 + (vv[t] >> 30);
-                                const uint32_t key = jj * kRingKeysPerSub + ((vv[t] >> kSlotShift) & 1023u);
+                                // key = (4 lo + (j & 3)) * 1024 + slot = lo << 12 | the entry's top
+                                // 12 bits (entries past the fill count as slot 0 of group lo)
+                                const uint32_t key = (lo << 12) + (((lim >> t) & 1u) ? (vv[t] >> kSlotShift) : 0u);
+                                atomicAnd(kbits + (key >> 5), ~(((fl[0] >> t) & 1u) << (key & 31)));
+                            }
+                        } else {
 #pragma unroll
-                                for (int f = 0; f < NFM; ++f)
-                                    if ((fl[f] >> t) & 1u) atomicAnd(kbits + f * kw + (key >> 5), ~(1u << (key & 31)));
+                            for (int t = 0; t < 4; ++t) {
+                                if ((any >> t) & 1u) {
+                                    if (r + t >= nxt) {
+                                        ++lo;
+                                        while (lo + 1 < nqs && pb[lo + 1] <= r + t) ++lo;
+                                        nxt = lo + 1 < nqs ? uint32_t(pb[lo + 1]) : 0xFFFFFFFFu;
+                                    }
+                                    // key = (4 lo + (j & 3)) * 1024 + slot = lo << 12 | the entry's top 12 bits
+                                    const uint32_t key = (lo << 12) + (vv[t] >> kSlotShift);
+#pragma unroll
+                                    for (int f = 0; f < NFM; ++f)
+                                        if ((fl[f] >> t) & 1u) atomicAnd(kbits + f * kw + (key >> 5), ~(1u << (key & 31)));
+                                }
                             }
                         }
                     }
@@ -571,8 +618,15 @@ __global__ void __launch_bounds__(512) k_gather_ring(TileMap tm, PartGeom pg, ui
     }
     lds_barrier();
     if (S > 1 || nf > 1) {
+#if PBF_HW_SLICES
+        // filter f, split sp: slice f * S + sp (k_hw_to_hitmask ANDs a filter's S slices)
+        for (uint32_t f = 0; f < nf; ++f)
+            for (uint32_t w = tid; w * 32 < nkeys; w += nt)
+                hw[(uint64_t(f) * S + sp) * neg_stride + (k0 >> 5) + w] = kbits[f * kw + w];
+#else
         for (uint32_t f = 0; f < nf; ++f)
             for (uint32_t w = tid; w * 32 < nkeys; w += nt) atomicAnd(hw + f * neg_stride + (k0 >> 5) + w, kbits[f * kw + w]);
+#endif
         return;
     }
     for (uint32_t w = tid; w * 32 < nkeys; w += nt) {

@@ -77,6 +77,23 @@ __device__ __forceinline__ uint4 ld_stream_nt(const uint32_t* p) {
 #ifndef PBF_NT_TILE
 #define PBF_NT_TILE 0
 #endif
+// gathers read a region quad's entries only when one of its result bits failed (the ring
+// gather of one filter: C2 probe 0.517 -> 0.504 ms; the counting-sort gather: neutral on C3, off)
+#ifndef PBF_GATHER_RFIRST
+#define PBF_GATHER_RFIRST 1
+#endif
+#ifndef PBF_GATHER_BRANCHFREE
+#define PBF_GATHER_BRANCHFREE 1
+#endif
+#ifndef PBF_GATHER_RFIRST_SORT
+#define PBF_GATHER_RFIRST_SORT 0
+#endif
+// PBF_HW_SLICES=1: gather splits write their words to their own slice of hw (k_hw_to_hitmask
+// ANDs the slices) instead of ANDing them into one word array with device-scope atomics.
+// Measured slower (C2 probe 0.504 vs 0.507 ms, C5 9.49 vs 9.61 ms: profiles/r02/s10/ab2_*): off.
+#ifndef PBF_HW_SLICES
+#define PBF_HW_SLICES 0
+#endif
 
 __device__ __forceinline__ uint4 ld_stream(const uint32_t* p) { return ld_stream_nt<PBF_NT_LOAD != 0>(p); }
 
@@ -557,7 +574,10 @@ __device__ __forceinline__ void tile_probe_body(uint32_t* smem, uint32_t b, cons
     const uint32_t lane = tid & 63, wave = tid >> 6, nwaves = nt >> 6;
     const uint32_t l = lane & 7, wsub = lane >> 3;  // piece of the word, word of the instruction
     const uint32_t stride = nwaves * 8;
-    constexpr int U = 8;  // instructions (8 words each) in flight per wave
+#ifndef PBF_TP_U
+#define PBF_TP_U 8
+#endif
+    constexpr int U = PBF_TP_U;  // instructions (8 words each) in flight per wave
     for (uint32_t c0 = wave * 8; c0 < total; c0 += stride * U) {
         uint4 v[U];
         uint32_t oo[U], lim[U];
@@ -636,7 +656,8 @@ __global__ void __launch_bounds__(1024) k_tile_probe_set(TileMap tm, PartGeom pg
 __global__ void __launch_bounds__(512) k_gather(TileMap tm, PartGeom pg, uint64_t n,
                                                 const uint32_t* __restrict__ regions, const uint32_t* __restrict__ R,
                                                 const uint32_t* __restrict__ subcnt, const uint32_t* __restrict__ neg,
-                                                uint8_t* __restrict__ hitmask, uint32_t* __restrict__ hw) {
+                                                uint8_t* __restrict__ hitmask, uint32_t* __restrict__ hw,
+                                                uint64_t hw_stride) {
     extern __shared__ uint32_t smem[];
     const uint32_t B = tm.nbuckets, cap = pg.cap, wpr = cap / 32, nsub = pg.nsub;
     const uint32_t tid = threadIdx.x, nt = blockDim.x;
@@ -701,9 +722,24 @@ __global__ void __launch_bounds__(512) k_gather(TileMap tm, PartGeom pg, uint64_
                 const uint32_t b = min(b0 + u * nwaves, b_hi - 1);
                 const uint32_t r = min(r0 + lane * 4, (max(fillb[u], 1u) - 1) & ~3u);
                 const uint64_t reg = region_id(g, b, pg.G, B);
+#if !PBF_GATHER_RFIRST_SORT
                 v[u] = ld_stream(regions + reg * cap + r);
+#endif
                 rw[u] = R[reg * wpr + (r >> 5)];
             }
+#if PBF_GATHER_RFIRST_SORT
+            // entries (for their key ids) only of quads with a failed result bit
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t b = b0 + u * nwaves;
+                const uint32_t r = r0 + lane * 4;
+                if (b < b_hi && r < fillb[u]) {
+                    uint32_t fails = ~r_quad(rw[u], r) & 0xFu;
+                    if (fillb[u] - r < 4) fails &= (1u << (fillb[u] - r)) - 1u;
+                    if (fails) v[u] = ld_stream(regions + region_id(g, b, pg.G, B) * cap + r);
+                }
+            }
+#endif
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const uint32_t b = b0 + u * nwaves;
@@ -735,8 +771,12 @@ __global__ void __launch_bounds__(512) k_gather(TileMap tm, PartGeom pg, uint64_
         }
     }
     lds_barrier();
-    if (S > 1) {  // AND this split's words into hw (k_hw_to_hitmask writes the hit mask)
+    if (S > 1) {  // this split's words into hw (k_hw_to_hitmask writes the hit mask)
+#if PBF_HW_SLICES
+        for (uint32_t w = tid; w * 32 < nkeys; w += nt) hw[sp * hw_stride + (k0 >> 5) + w] = kbits[w];
+#else
         for (uint32_t w = tid; w * 32 < nkeys; w += nt) atomicAnd(hw + (k0 >> 5) + w, kbits[w]);
+#endif
         return;
     }
     // hit-mask words for keys [k0, k1): k0 is a multiple of 64
@@ -751,12 +791,15 @@ __global__ void __launch_bounds__(512) k_gather(TileMap tm, PartGeom pg, uint64_
     }
 }
 
-// hw (ANDed gather words, one per 32 keys) → the LSB-first hit mask of n keys.
-__global__ void k_hw_to_hitmask(const uint32_t* __restrict__ hw, uint64_t n, uint8_t* __restrict__ hitmask) {
+// hw (gather words, one per 32 keys; S slices `stride` words apart, ANDed) → the LSB-first hit
+// mask of n keys.
+__global__ void k_hw_to_hitmask(const uint32_t* __restrict__ hw, uint64_t n, uint8_t* __restrict__ hitmask,
+                                uint32_t S, uint64_t stride) {
     const uint64_t nw = (n + 31) / 32;
     for (uint64_t w = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; w < nw; w += uint64_t(gridDim.x) * blockDim.x) {
         const uint64_t key0 = w * 32;
-        const uint32_t bits = hw[w];
+        uint32_t bits = hw[w];
+        for (uint32_t q = 1; q < S; ++q) bits &= hw[q * stride + w];
         const uint64_t nbt = min<uint64_t>(4, (n - key0 + 7) / 8);
         if (nbt == 4 && (reinterpret_cast<uintptr_t>(hitmask + key0 / 8) & 3) == 0)
             *reinterpret_cast<uint32_t*>(hitmask + key0 / 8) = bits;

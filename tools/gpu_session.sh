@@ -140,6 +140,18 @@ for step in "$@"; do
              for G in 256 512; do PBF_PART_G=$G run c2_G$G 300 python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-host-inclusive; done ;;
     gpacked) for r in 1 2; do for pk in 0 1; do PBF_GATHER_PACKED=$pk run gp${pk}_c2_$r 300 python bench.py --steps 40 --warmup 5 --no-cpu-baseline --no-host-inclusive; done; done
              for pk in 0 1; do PBF_GATHER_PACKED=$pk run gp${pk}_c5 300 python bench.py --config c5 --steps 5 --warmup 2 --no-cpu-baseline --no-host-c5; done ;;
+    direct) for s1 in 1 2 6; do PBF_PROBE_S1=$s1 run direct_s1_$s1 300 python bench.py --steps 40 --warmup 5 --probe-mode 1 --no-cpu-baseline --no-host-inclusive; done
+            run prof_direct 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_direct -o run -- python bench.py --steps 20 --warmup 5 --probe-mode 1 --no-cpu-baseline --no-host-inclusive
+            python tools/prof_summary.py gpurun_out/prof_direct > gpurun_out/prof_direct_summary.txt 2>&1 || true ;;
+    ab) # A/B: the default library against every build/variants/*.so, alternating, PBF_AB_ARGS for the bench
+        for r in 1 2; do
+          run ab_default_$r 300 python bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-host-inclusive ${PBF_AB_ARGS:-}
+          for v in build/variants/*.so; do nm=$(basename $v .so); PBF_LIB=$PWD/$v run ab_${nm}_$r 300 python bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-host-inclusive ${PBF_AB_ARGS:-}; done
+        done ;;
+    ab_c5) run abc5_default 300 python bench.py --config c5 --steps 5 --warmup 2 --no-cpu-baseline --no-host-c5
+           for v in build/variants/*.so; do nm=$(basename $v .so); PBF_LIB=$PWD/$v run abc5_${nm} 300 python bench.py --config c5 --steps 5 --warmup 2 --no-cpu-baseline --no-host-c5; done ;;
+    ab_c3) run abc3_default 300 python bench.py --config c3 --steps 3 --warmup 1 --no-cpu-baseline --no-host-inclusive
+           for v in build/variants/*.so; do nm=$(basename $v .so); PBF_LIB=$PWD/$v run abc3_${nm} 300 python bench.py --config c3 --steps 3 --warmup 1 --no-cpu-baseline --no-host-inclusive; done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
