@@ -498,7 +498,7 @@ __global__ void __launch_bounds__(512) k_gather_ring(TileMap tm, PartGeom pg, ui
             }
         }
     }
-    constexpr int U = 4;
+    constexpr int U = PBF_GATHER_U;  // regions in flight per wave
     for (uint32_t b0 = b_lo + wave; !packed && b0 < b_hi; b0 += nwaves * U) {
         uint32_t fillb[U];
 #pragma unroll

@@ -82,8 +82,14 @@ __device__ __forceinline__ uint4 ld_stream_nt(const uint32_t* p) {
 #ifndef PBF_GATHER_RFIRST
 #define PBF_GATHER_RFIRST 1
 #endif
+// PBF_GATHER_BRANCHFREE=1: the one-filter ring gather issues all 4 ANDs of a failed quad
+// (passed entries with all-ones masks) instead of branching per entry.  Measured slower (C2
+// probe 0.5145 vs 0.5004 ms, profiles/r02/s10/ab3_*): off.
 #ifndef PBF_GATHER_BRANCHFREE
-#define PBF_GATHER_BRANCHFREE 1
+#define PBF_GATHER_BRANCHFREE 0
+#endif
+#ifndef PBF_GATHER_U
+#define PBF_GATHER_U 4
 #endif
 #ifndef PBF_GATHER_RFIRST_SORT
 #define PBF_GATHER_RFIRST_SORT 0
