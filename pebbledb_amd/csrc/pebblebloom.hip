@@ -130,6 +130,20 @@ uint64_t probe_chunk() {
     return v;
 }
 
+// Overlapped probe pipelines (PBF_PROBE_OVERLAP = chunk count >= 2; 0/1 = one pipeline): the
+// batch is cut into chunks whose pipelines alternate between the filter's stream and a side
+// stream, each with its own scratch set; chunk c's partition (instruction-bound) starts when
+// chunk c-1's partition is done, so it runs beside chunk c-1's tile test and gather
+// (memory-bound).
+uint32_t probe_overlap() {
+    static const uint32_t v = [] {
+        const char* e = std::getenv("PBF_PROBE_OVERLAP");
+        const int x = e ? std::atoi(e) : 0;
+        return x >= 2 ? uint32_t(std::min(x, 16)) : 0u;
+    }();
+    return v;
+}
+
 // Words loaded in the probe's first stage (PBF_PROBE_S1 overrides; tuning knob).
 int probe_stage1() {
     static const int v = [] {
@@ -313,6 +327,8 @@ struct pbf_filter {
     Scratch* sc = nullptr;           // leased for the current call
     uint64_t* dpop = nullptr;
     hipEvent_t ev = nullptr;       // stream joins of multi-filter probes
+    hipEvent_t ev_part = nullptr;  // overlapped probe chunks: partition done / side stream joins
+    hipEvent_t ev_side = nullptr;
     std::mutex mu;                 // one host thread inside the handle at a time
 };
 
@@ -469,10 +485,64 @@ hipError_t pooled_stream(int device, hipStream_t* out) {
     return hipSuccess;
 }
 
+// One extra stream per device for the overlapped probe chunks (created on first use).
+hipError_t side_stream(int device, hipStream_t* out) {
+    static std::mutex mu;
+    static std::map<int, hipStream_t> side;
+    std::lock_guard<std::mutex> lock(mu);
+    auto it = side.find(device);
+    if (it == side.end()) {
+        hipStream_t st = nullptr;
+        const hipError_t e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
+        if (e != hipSuccess) return e;
+        it = side.emplace(device, st).first;
+    }
+    *out = it->second;
+    return hipSuccess;
+}
+
 // Lease a scratch set of f's device for work enqueued on f's stream (RAII).  Prefers a set
 // whose previous work is done or was on this same stream; creates one while fewer than
 // max_scratch_sets() exist; otherwise takes a free set and orders this stream after its
 // previous user.
+Scratch* pick_set(int device, hipStream_t st) {
+    DevicePool& pool = device_pool(device);
+    std::lock_guard<std::mutex> lock(pool.mu);
+    Scratch* any = nullptr;
+    for (Scratch* s : pool.sets) {
+        if (s->leased) continue;
+        if (!any) any = s;
+        if (!s->last || s->last_stream == st || event_done(s->last)) {
+            s->leased = true;
+            return s;
+        }
+    }
+    Scratch* pick = nullptr;
+    if (pool.sets.size() < max_scratch_sets() || !any) {
+        pick = new Scratch();
+        pool.sets.push_back(pick);
+    }
+    if (!pick) pick = any;
+    pick->leased = true;
+    return pick;
+}
+
+// A second set for work on another stream `st` (released with return_set on that stream).
+int lease_set(int device, hipStream_t st, Scratch** out) {
+    Scratch* s = pick_set(device, st);
+    *out = s;
+    if (!s->last) HIP_TRY(hipEventCreateWithFlags(&s->last, hipEventDisableTiming));
+    if (s->last_stream && s->last_stream != st) HIP_TRY(hipStreamWaitEvent(st, s->last, 0));
+    return PBF_OK;
+}
+
+void return_set(int device, Scratch* s, hipStream_t st) {
+    if (hipEventRecord(s->last, st) == hipSuccess) s->last_stream = st;
+    DevicePool& pool = device_pool(device);
+    std::lock_guard<std::mutex> lock(pool.mu);
+    s->leased = false;
+}
+
 class Lease {
    public:
     Lease(pbf_filter_t* f) : f_(f) {}
@@ -893,8 +963,12 @@ int run_tiled(pbf_filter_t* f, const Batch& b) {
 // keys are hashed and partitioned once, on f's stream with f's scratch (f = the set's first
 // filter, also for every later group of a large set); the tile test and the gather then run
 // once per filter.  hitmasks[i] + hm_off is filter i's output.
+// sc_ / st_: another scratch set and stream than f's (the overlapped chunks of probe_device);
+// after_part: recorded on the stream right after the partition launch.
 int run_tiled_probe_set(pbf_filter_t* f, pbf_filter_t* const* fs, uint32_t nf, const Batch& b,
-                        uint8_t* const* hitmasks, uint64_t hm_off) {
+                        uint8_t* const* hitmasks, uint64_t hm_off, Scratch* sc_ = nullptr,
+                        hipStream_t st_ = nullptr, hipEvent_t after_part = nullptr) {
+    Scratch* const sc = sc_ ? sc_ : f->sc;
     const TileMap& tm = f->tm;
     const uint32_t B = tm.nbuckets;
     const uint32_t k = f->k;
@@ -902,29 +976,29 @@ int run_tiled_probe_set(pbf_filter_t* f, pbf_filter_t* const* fs, uint32_t nf, c
     const PartGeom& pg = pl.pg;
     const uint32_t nfg = pg.ring ? nf : 1;  // filters per gather launch (R and hw copies)
     f->last_probe_detail = (pg.ring ? PBF_DETAIL_RING : PBF_DETAIL_SORT) | (nfg << 8);
-    HIP_TRY(f->sc->regions.ensure(size_t(pg.G) * B * pg.cap * 4));
-    HIP_TRY(f->sc->fill.ensure(size_t(pg.G) * B * 4));
+    HIP_TRY(sc->regions.ensure(size_t(pg.G) * B * pg.cap * 4));
+    HIP_TRY(sc->fill.ensure(size_t(pg.G) * B * 4));
     // sort partition: per-sub-chunk tile counts; ring partition: cumulative counts per 4 sub-chunks
-    HIP_TRY(f->sc->subcnt.ensure(pg.ring ? size_t(pg.G) * B * (pg.nq + 1) * 4 : size_t(pg.G) * pg.nsub * B * 4));
+    HIP_TRY(sc->subcnt.ensure(pg.ring ? size_t(pg.G) * B * (pg.nq + 1) * 4 : size_t(pg.G) * pg.nsub * B * 4));
     const size_t r_words = size_t(pg.G) * B * (pg.cap / 32);
-    HIP_TRY(f->sc->rbits.ensure(r_words * 4 * nfg));
+    HIP_TRY(sc->rbits.ensure(r_words * 4 * nfg));
     const uint64_t neg_words = (b.n + 31) / 32;
     const size_t neg_bytes = neg_words * 4;
-    HIP_TRY(f->sc->neg.ensure(neg_bytes * nf));
-    auto* regions = static_cast<uint32_t*>(f->sc->regions.p);
-    auto* fill = static_cast<uint32_t*>(f->sc->fill.p);
-    auto* subcnt = static_cast<uint32_t*>(f->sc->subcnt.p);
-    auto* R = static_cast<uint32_t*>(f->sc->rbits.p);
-    auto* neg = static_cast<uint32_t*>(f->sc->neg.p);
-    hipStream_t s = f->stream;
+    HIP_TRY(sc->neg.ensure(neg_bytes * nf));
+    auto* regions = static_cast<uint32_t*>(sc->regions.p);
+    auto* fill = static_cast<uint32_t*>(sc->fill.p);
+    auto* subcnt = static_cast<uint32_t*>(sc->subcnt.p);
+    auto* R = static_cast<uint32_t*>(sc->rbits.p);
+    auto* neg = static_cast<uint32_t*>(sc->neg.p);
+    hipStream_t s = st_ ? st_ : f->stream;
     // gather split over S tile ranges (several small workgroups per CU)
     const uint32_t S = pl.gsplit;
     const bool use_hw = S > 1 || nfg > 1;
     uint32_t* hw = nullptr;
     if (use_hw) {
         // PBF_HW_SLICES: one slice of words per (filter, gather split), ANDed by k_hw_to_hitmask
-        HIP_TRY(f->sc->hw.ensure(neg_bytes * nfg * (PBF_HW_SLICES ? S : 1)));
-        hw = static_cast<uint32_t*>(f->sc->hw.p);
+        HIP_TRY(sc->hw.ensure(neg_bytes * nfg * (PBF_HW_SLICES ? S : 1)));
+        hw = static_cast<uint32_t*>(sc->hw.p);
     }
     ProbeSet ps{};
     ps.nf = nf;
@@ -972,6 +1046,7 @@ int run_tiled_probe_set(pbf_filter_t* f, pbf_filter_t* const* fs, uint32_t nf, c
         });
         HIP_TRY(err);
         CHECK_LAUNCH();
+        if (after_part) HIP_TRY(hipEventRecord(after_part, s));
         auto gring = nf > 1 ? k_gather_ring<kMaxProbeSet> : k_gather_ring<1>;
         if (pg.ring) HIP_TRY(allow_lds(gring, pl.lds_gather));
         else HIP_TRY(allow_lds(k_gather, pl.lds_gather));
@@ -1017,8 +1092,8 @@ int run_tiled_probe_set(pbf_filter_t* f, pbf_filter_t* const* fs, uint32_t nf, c
     };
     if (nf > 1 || !pg.ring || k < 2 || probe_rounds() < 2) return round(0, k, nullptr, hitmasks);
     // two rounds: seed 0 for every key, then seeds 1..k-1 for the keys seed 0 left alive
-    HIP_TRY(f->sc->alive.ensure(neg_bytes));
-    auto* alive = static_cast<uint32_t*>(f->sc->alive.p);
+    HIP_TRY(sc->alive.ensure(neg_bytes));
+    auto* alive = static_cast<uint32_t*>(sc->alive.p);
     uint8_t* alive_out[1] = {reinterpret_cast<uint8_t*>(alive)};
     const uint64_t keep_off = hm_off;
     hm_off = 0;
@@ -1096,12 +1171,55 @@ int add_device(pbf_filter_t* f, const Batch& b) {
     return run_atomic(f, b);
 }
 
+// C chunks of a tiled probe (see probe_overlap): chunk c runs on stream c % 2 (f's stream or the
+// device's side stream) with that stream's scratch set; its partition waits for chunk c-1's.
+int probe_overlapped(pbf_filter_t* f, const Batch& b, uint8_t* hitmask_dev, uint32_t C) {
+    hipStream_t side = nullptr;
+    HIP_TRY(side_stream(f->device, &side));
+    if (!f->ev_part) HIP_TRY(hipEventCreateWithFlags(&f->ev_part, hipEventDisableTiming));
+    if (!f->ev_side) HIP_TRY(hipEventCreateWithFlags(&f->ev_side, hipEventDisableTiming));
+    // the side stream starts after everything already queued on f's stream (keys, builds)
+    HIP_TRY(hipEventRecord(f->ev_side, f->stream));
+    HIP_TRY(hipStreamWaitEvent(side, f->ev_side, 0));
+    Scratch* sc2 = nullptr;
+    int rc = lease_set(f->device, side, &sc2);
+    if (rc) return rc;
+    const uint64_t per = (((b.n + C - 1) / C) + 63) & ~uint64_t(63);
+    pbf_filter_t* fs[1] = {f};
+    uint32_t c = 0;
+    for (uint64_t i0 = 0; i0 < b.n && rc == PBF_OK; i0 += per, ++c) {
+        Batch cb = b;
+        cb.n = std::min<uint64_t>(per, b.n - i0);
+        if (b.km == kVar)
+            cb.ks.offsets = b.ks.offsets + i0;
+        else
+            cb.ks.data = b.ks.data + i0 * b.ks.key_len;
+        const bool on_side = c & 1;
+        hipStream_t st = on_side ? side : f->stream;
+        if (c > 0) {  // after the previous chunk's partition
+            const hipError_t e = hipStreamWaitEvent(st, f->ev_part, 0);
+            if (e != hipSuccess) { rc = fail(PBF_ERR_HIP, hipGetErrorString(e)); break; }
+        }
+        uint8_t* outs[1] = {hitmask_dev + i0 / 8};
+        rc = run_tiled_probe_set(f, fs, 1, cb, outs, 0, on_side ? sc2 : f->sc, st, f->ev_part);
+    }
+    // f's stream joins the side stream; the side set's next user orders after this call
+    return_set(f->device, sc2, side);
+    if (rc) return rc;
+    HIP_TRY(hipEventRecord(f->ev_side, side));
+    HIP_TRY(hipStreamWaitEvent(f->stream, f->ev_side, 0));
+    f->last_probe_mode = PBF_PROBE_TILED;
+    return PBF_OK;
+}
+
 int probe_device(pbf_filter_t* f, const Batch& b, uint8_t* hitmask_dev) {
     if (b.n == 0) return PBF_OK;
     int rc = materialise(f);
     if (rc) return rc;
     if (want_tiled_probe(f, b.n)) {
         const uint64_t per = tiled_probe_batch(f, b.km);
+        const uint32_t C = probe_overlap();
+        if (C >= 2 && b.n >= uint64_t(C) << 20 && b.n <= per) return probe_overlapped(f, b, hitmask_dev, C);
         for (uint64_t i0 = 0; i0 < b.n; i0 += per) {
             Batch c = b;
             c.n = std::min<uint64_t>(per, b.n - i0);
@@ -1593,6 +1711,8 @@ int pbf_destroy(pbf_filter_t* f) {
     }
     if (f->bitmap) bitmap_release(f->device, bitmap_alloc_bytes(f->alloc_words), f->bitmap);
     if (f->ev) (void)hipEventDestroy(f->ev);
+    if (f->ev_part) (void)hipEventDestroy(f->ev_part);
+    if (f->ev_side) (void)hipEventDestroy(f->ev_side);
     delete f;  // the stream belongs to the device's pool
     return PBF_OK;
 }
