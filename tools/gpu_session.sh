@@ -154,6 +154,7 @@ for step in "$@"; do
            for v in build/variants/*.so; do nm=$(basename $v .so); PBF_LIB=$PWD/$v run abc3_${nm} 300 python bench.py --config c3 --steps 3 --warmup 1 --no-cpu-baseline --no-host-inclusive; done ;;
     overlap) for r in 1 2; do for c in 0 2 3 4; do PBF_PROBE_OVERLAP=$c run ov${c}_$r 300 python bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-host-inclusive; done; done ;;
     overlap_parity) PBF_PROBE_OVERLAP=3 run ov_parity 600 python -u -m pytest tests/test_gpu_device_resident.py tests/test_gpu_parity.py -m gpu -x -q -rf --timeout 150 --timeout-method thread ;;
+    parity_var) for v in build/variants/*.so; do nm=$(basename $v .so); PBF_LIB=$PWD/$v run parity_$nm 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_device_resident.py tests/test_gpu_multi.py -m gpu -x -q -rf --timeout 300 --timeout-method thread; done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
