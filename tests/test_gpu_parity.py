@@ -457,3 +457,45 @@ def test_bits_outside_the_bitmap_are_dropped_like_to_bytes():
     neg = BloomFilter(4, 2, bits=-1)
     assert neg.to_bytes() == b"\xff\xff\xff\xff\x02"
     assert neg.may_contain("anything") and neg.may_contain("")
+
+
+_OVERLAP_CHILD = """
+import sys; sys.path.insert(0, '.')
+import numpy as np
+from pebbledb_amd import BloomFilter, PackedKeys
+from pebbledb_amd.keys import splitmix_hex_keys, varlen_keys
+from oracle.oracle import COracle
+o = COracle()
+members = PackedKeys.fixed(splitmix_hex_keys(41, 0, 2_000_000))
+# 4M + 37 probe keys: members, absent keys and a ragged tail (chunks of ceil(n / C) rounded to 64)
+q = PackedKeys.fixed(np.concatenate([splitmix_hex_keys(41, 1_000_000, 2_000_000),
+                                     splitmix_hex_keys(42, 0, 2_000_037)]))
+d, off = varlen_keys(43, 0, 3_300_001)
+vq = PackedKeys(d, 3_300_001, offsets=off)  # >= 3 * 2^20: the 3-chunk split applies
+for nb, k in ((2 ** 27, 6), (3 * 2 ** 25 + 3, 7)):
+    want = o.build(nb, k, members, omp=True)
+    bf = BloomFilter(nb, k); bf.add_many(members)
+    assert bf.bitmap() == want.tobytes(), nb
+    bf.set_probe_mode(2)
+    for keys in (q, vq):
+        got = bf.may_contain_many(keys, packed=True)
+        assert bf.last_probe_mode == 2
+        assert np.array_equal(got, o.probe(want, k, keys, omp=True)), (nb, keys.n)
+print('ok')
+"""
+
+
+@pytest.mark.parametrize("chunks", ["2", "3"])
+def test_overlapped_probe_chunks(chunks):
+    """PBF_PROBE_OVERLAP (opt-in, measured slower on C2): the tiled probe cut into chunks whose
+    pipelines alternate between the filter's stream and a side stream with their own scratch
+    sets, each partition ordered after the previous one.  Hit masks equal the oracle's for
+    fixed and variable-length keys, ragged chunk tails, power-of-two and odd m (child process:
+    the switch is read once per process)."""
+    import os
+    import subprocess
+    import sys
+    env = dict(os.environ, PBF_PROBE_OVERLAP=chunks)
+    r = subprocess.run([sys.executable, "-c", _OVERLAP_CHILD], env=env, capture_output=True, text=True, timeout=300,
+                       cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
