@@ -155,6 +155,10 @@ for step in "$@"; do
     overlap) for r in 1 2; do for c in 0 2 3 4; do PBF_PROBE_OVERLAP=$c run ov${c}_$r 300 python bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-host-inclusive; done; done ;;
     overlap_parity) PBF_PROBE_OVERLAP=3 run ov_parity 600 python -u -m pytest tests/test_gpu_device_resident.py tests/test_gpu_parity.py -m gpu -x -q -rf --timeout 150 --timeout-method thread ;;
     parity_var) for v in build/variants/*.so; do nm=$(basename $v .so); PBF_LIB=$PWD/$v run parity_$nm 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_device_resident.py tests/test_gpu_multi.py -m gpu -x -q -rf --timeout 300 --timeout-method thread; done ;;
+    halves) for r in 1 2; do for h in 2 1; do PBF_RING_HALVES=$h run hv${h}_$r 300 python bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-host-inclusive; done; done
+            for h in 2 1; do PBF_RING_HALVES=$h run hvc5_$h 300 python bench.py --config c5 --steps 5 --warmup 2 --no-cpu-baseline --no-host-c5; done ;;
+    rtime2) for b in ring_time ring_time_nostore ring_time_noappend ring_time_hashonly ring_time_synth_hashonly; do run $b 300 tools/microbench/$b; done ;;
+    rtime3) for b in ring_time ring_time_noappend ring_time_hashonly; do run $b 300 tools/microbench/$b; done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
