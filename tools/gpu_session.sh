@@ -159,6 +159,7 @@ for step in "$@"; do
             for h in 2 1; do PBF_RING_HALVES=$h run hvc5_$h 300 python bench.py --config c5 --steps 5 --warmup 2 --no-cpu-baseline --no-host-c5; done ;;
     rtime2) for b in ring_time ring_time_nostore ring_time_noappend ring_time_hashonly ring_time_synth_hashonly; do run $b 300 tools/microbench/$b; done ;;
     rtime3) for b in ring_time ring_time_noappend ring_time_hashonly; do run $b 300 tools/microbench/$b; done ;;
+    c4ab) for r in 1 2; do for lg in 31 30; do PBF_BUILD_POSITIONS_LOG2=$lg run c4ab_${lg}_$r 400 python bench.py --config c4 --steps 3 --warmup 1 --no-cpu-baseline; done; done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
