@@ -530,8 +530,8 @@ __global__ void __launch_bounds__(512) k_gather_ring(TileMap tm, PartGeom pg, ui
             // needed) are loaded only when one of its entries failed, so quads that passed (a
             // probe batch's members) cost their result bits alone.  Multi-filter sets: nearly
             // every quad fails some filter, so entries and result words go out together.
+            uint32_t anyq[U];  // one filter: the quad's failed entries as byte-spread bits (0: skip)
             if constexpr (PBF_GATHER_RFIRST && NFM == 1) {
-                uint32_t anyq[U];
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
                     const uint32_t b = min(b0 + u * nwaves, b_hi - 1);
@@ -544,8 +544,10 @@ __global__ void __launch_bounds__(512) k_gather_ring(TileMap tm, PartGeom pg, ui
                     const uint32_t r = r0 + lane * 4;
                     uint32_t a = 0;
                     if (b < b_hi && r < fillb[u]) {
-                        const uint32_t lim = fillb[u] - r < 4 ? (1u << (fillb[u] - r)) - 1u : 0xFu;
-                        a = ~r_quad(rw[0][u], r) & lim;
+                        // the quad's 4 result bits sit at bits 0, 8, 16, 24 after the shift (see
+                        // r_quad); entries past the fill masked off, no compaction needed here
+                        const uint32_t cnt = min(fillb[u] - r, 4u);
+                        a = (~rw[0][u] >> ((r & 31) >> 2)) & (0x01010101u >> (32 - 8 * cnt));
                     }
                     anyq[u] = a;
                 }
@@ -555,6 +557,7 @@ __global__ void __launch_bounds__(512) k_gather_ring(TileMap tm, PartGeom pg, ui
             } else {
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
+                    anyq[u] = 1u;
                     const uint32_t b = min(b0 + u * nwaves, b_hi - 1);
                     const uint32_t r = min(r0 + lane * 4, (max(fillb[u], 1u) - 1) & ~3u);
                     v[u] = ld_stream(entries_at(b, r));
@@ -567,12 +570,14 @@ __global__ void __launch_bounds__(512) k_gather_ring(TileMap tm, PartGeom pg, ui
             for (int u = 0; u < U; ++u) {
                 const uint32_t b = b0 + u * nwaves;
                 const uint32_t r = r0 + lane * 4;
-                if (b < b_hi && r < fillb[u]) {
-                    const uint32_t lim = fillb[u] - r < 4 ? (1u << (fillb[u] - r)) - 1u : 0xFu;
+                if (anyq[u] && b < b_hi && r < fillb[u]) {
+                    // failed entries as byte-spread bits: entry r + t at bit 8t (the result word
+                    // shifted to the quad's piece, see r_quad; no compaction multiply)
+                    const uint32_t lim = 0x01010101u >> (32 - 8 * min(fillb[u] - r, 4u));
                     uint32_t fl[NFM], any = 0;
 #pragma unroll
                     for (int f = 0; f < NFM; ++f) {
-                        fl[f] = uint32_t(f) < nf ? (~r_quad(rw[f][u], r) & lim) : 0u;
+                        fl[f] = uint32_t(f) < nf ? ((~rw[f][u] >> ((r & 31) >> 2)) & lim) : 0u;
                         any |= fl[f];
                     }
                     if (any) {
@@ -607,13 +612,13 @@ __global__ void __launch_bounds__(512) k_gather_ring(TileMap tm, PartGeom pg, ui
                                 }
                                 // key = (4 lo + (j & 3)) * 1024 + slot = lo << 12 | the entry's top
                                 // 12 bits (entries past the fill count as slot 0 of group lo)
-                                const uint32_t key = (lo << 12) + (((lim >> t) & 1u) ? (vv[t] >> kSlotShift) : 0u);
-                                atomicAnd(kbits + (key >> 5), ~(((fl[0] >> t) & 1u) << (key & 31)));
+                                const uint32_t key = (lo << 12) + (((lim >> (8 * t)) & 1u) ? (vv[t] >> kSlotShift) : 0u);
+                                atomicAnd(kbits + (key >> 5), ~(((fl[0] >> (8 * t)) & 1u) << (key & 31)));
                             }
                         } else {
 #pragma unroll
                             for (int t = 0; t < 4; ++t) {
-                                if ((any >> t) & 1u) {
+                                if ((any >> (8 * t)) & 1u) {
                                     if (r + t >= nxt) {
                                         ++lo;
                                         while (lo + 1 < nqs && pb[lo + 1] <= r + t) ++lo;
@@ -623,7 +628,7 @@ __global__ void __launch_bounds__(512) k_gather_ring(TileMap tm, PartGeom pg, ui
                                     const uint32_t key = (lo << 12) + (vv[t] >> kSlotShift);
 #pragma unroll
                                     for (int f = 0; f < NFM; ++f)
-                                        if ((fl[f] >> t) & 1u) atomicAnd(kbits + f * kw + (key >> 5), ~(1u << (key & 31)));
+                                        if ((fl[f] >> (8 * t)) & 1u) atomicAnd(kbits + f * kw + (key >> 5), ~(1u << (key & 31)));
                                 }
                             }
                         }
