@@ -996,8 +996,7 @@ int run_tiled_probe_set(pbf_filter_t* f, pbf_filter_t* const* fs, uint32_t nf, c
     const bool use_hw = S > 1 || nfg > 1;
     uint32_t* hw = nullptr;
     if (use_hw) {
-        // PBF_HW_SLICES: one slice of words per (filter, gather split), ANDed by k_hw_to_hitmask
-        HIP_TRY(sc->hw.ensure(neg_bytes * nfg * (PBF_HW_SLICES ? S : 1)));
+        HIP_TRY(sc->hw.ensure(neg_bytes * nfg));
         hw = static_cast<uint32_t*>(sc->hw.p);
     }
     ProbeSet ps{};
@@ -1031,7 +1030,7 @@ int run_tiled_probe_set(pbf_filter_t* f, pbf_filter_t* const* fs, uint32_t nf, c
                             if (err == hipSuccess)
                                 kern<<<pg.G, kPartThreads, pl.lds_part, s>>>(b.ks, b.n, int(kr), tm, pg, regions,
                                                                      fill, subcnt, nullptr, nullptr, ps, sbase,
-                                                                     alive, use_hw && !PBF_HW_SLICES ? hw : nullptr);
+                                                                     alive, use_hw ? hw : nullptr);
                         });
                     }
                 } else {
@@ -1067,24 +1066,22 @@ int run_tiled_probe_set(pbf_filter_t* f, pbf_filter_t* const* fs, uint32_t nf, c
             CHECK_LAUNCH();
             if (use_hw) {
                 for (uint32_t i = 0; i < nf; ++i) {
-                    const uint32_t ns = PBF_HW_SLICES ? S : 1;
-                    k_hw_to_hitmask<<<grid_for(neg_words, 256, 4096), 256, 0, s>>>(hw + uint64_t(i) * ns * neg_words,
-                                                                                   b.n, outs[i] + hm_off, ns, neg_words);
+                    k_hw_to_hitmask<<<grid_for(neg_words, 256, 4096), 256, 0, s>>>(hw + i * neg_words, b.n,
+                                                                                   outs[i] + hm_off);
                     CHECK_LAUNCH();
                 }
             }
             return PBF_OK;
         }
         for (uint32_t i = 0; i < nf; ++i) {
-            if (S > 1 && !PBF_HW_SLICES) HIP_TRY(hipMemsetAsync(hw, 0xFF, neg_bytes, s));
+            if (S > 1) HIP_TRY(hipMemsetAsync(hw, 0xFF, neg_bytes, s));
             tprobe<<<B, 1024, lds_tile, s>>>(tm, pg, regions, fill, fs[i]->bitmap, R);
             CHECK_LAUNCH();
             k_gather<<<grid, 512, pl.lds_gather, s>>>(tm, pg, b.n, regions, R, subcnt, neg + i * neg_words,
-                                                      outs[i] + hm_off, hw, neg_words);
+                                                      outs[i] + hm_off, hw);
             CHECK_LAUNCH();
             if (S > 1) {
-                k_hw_to_hitmask<<<grid_for(neg_words, 256, 4096), 256, 0, s>>>(hw, b.n, outs[i] + hm_off,
-                                                                               PBF_HW_SLICES ? S : 1, neg_words);
+                k_hw_to_hitmask<<<grid_for(neg_words, 256, 4096), 256, 0, s>>>(hw, b.n, outs[i] + hm_off);
                 CHECK_LAUNCH();
             }
         }

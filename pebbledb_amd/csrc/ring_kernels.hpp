@@ -599,37 +599,19 @@ __global__ void __launch_bounds__(512) k_gather_ring(TileMap tm, PartGeom pg, ui
                         // the next group's first entry: a boundary inside the quad is rare (a
                         // group holds ~24 entries at C2), so entries usually take lo with one compare
                         uint32_t nxt = lo + 1 < nqs ? uint32_t(pb[lo + 1]) : 0xFFFFFFFFu;
-                        if constexpr (NFM == 1 && PBF_GATHER_BRANCHFREE) {
-                            // one filter: every entry of a failed quad issues its AND, a passed
-                            // entry's with an all-ones mask (most failed quads fail whole: their
-                            // keys are non-members), so the quad takes no per-entry branches
 #pragma unroll
-                            for (int t = 0; t < 4; ++t) {
+                        for (int t = 0; t < 4; ++t) {
+                            if ((any >> (8 * t)) & 1u) {
                                 if (r + t >= nxt) {
                                     ++lo;
                                     while (lo + 1 < nqs && pb[lo + 1] <= r + t) ++lo;
                                     nxt = lo + 1 < nqs ? uint32_t(pb[lo + 1]) : 0xFFFFFFFFu;
                                 }
-                                // key = (4 lo + (j & 3)) * 1024 + slot = lo << 12 | the entry's top
-                                // 12 bits (entries past the fill count as slot 0 of group lo)
-                                const uint32_t key = (lo << 12) + (((lim >> (8 * t)) & 1u) ? (vv[t] >> kSlotShift) : 0u);
-                                atomicAnd(kbits + (key >> 5), ~(((fl[0] >> (8 * t)) & 1u) << (key & 31)));
-                            }
-                        } else {
+                                // key = (4 lo + (j & 3)) * 1024 + slot = lo << 12 | the entry's top 12 bits
+                                const uint32_t key = (lo << 12) + (vv[t] >> kSlotShift);
 #pragma unroll
-                            for (int t = 0; t < 4; ++t) {
-                                if ((any >> (8 * t)) & 1u) {
-                                    if (r + t >= nxt) {
-                                        ++lo;
-                                        while (lo + 1 < nqs && pb[lo + 1] <= r + t) ++lo;
-                                        nxt = lo + 1 < nqs ? uint32_t(pb[lo + 1]) : 0xFFFFFFFFu;
-                                    }
-                                    // key = (4 lo + (j & 3)) * 1024 + slot = lo << 12 | the entry's top 12 bits
-                                    const uint32_t key = (lo << 12) + (vv[t] >> kSlotShift);
-#pragma unroll
-                                    for (int f = 0; f < NFM; ++f)
-                                        if ((fl[f] >> (8 * t)) & 1u) atomicAnd(kbits + f * kw + (key >> 5), ~(1u << (key & 31)));
-                                }
+                                for (int f = 0; f < NFM; ++f)
+                                    if ((fl[f] >> (8 * t)) & 1u) atomicAnd(kbits + f * kw + (key >> 5), ~(1u << (key & 31)));
                             }
                         }
                     }
@@ -639,15 +621,8 @@ __global__ void __launch_bounds__(512) k_gather_ring(TileMap tm, PartGeom pg, ui
     }
     lds_barrier();
     if (S > 1 || nf > 1) {
-#if PBF_HW_SLICES
-        // filter f, split sp: slice f * S + sp (k_hw_to_hitmask ANDs a filter's S slices)
-        for (uint32_t f = 0; f < nf; ++f)
-            for (uint32_t w = tid; w * 32 < nkeys; w += nt)
-                hw[(uint64_t(f) * S + sp) * neg_stride + (k0 >> 5) + w] = kbits[f * kw + w];
-#else
         for (uint32_t f = 0; f < nf; ++f)
             for (uint32_t w = tid; w * 32 < nkeys; w += nt) atomicAnd(hw + f * neg_stride + (k0 >> 5) + w, kbits[f * kw + w]);
-#endif
         return;
     }
     for (uint32_t w = tid; w * 32 < nkeys; w += nt) {

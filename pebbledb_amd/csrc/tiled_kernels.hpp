@@ -82,23 +82,11 @@ __device__ __forceinline__ uint4 ld_stream_nt(const uint32_t* p) {
 #ifndef PBF_GATHER_RFIRST
 #define PBF_GATHER_RFIRST 1
 #endif
-// PBF_GATHER_BRANCHFREE=1: the one-filter ring gather issues all 4 ANDs of a failed quad
-// (passed entries with all-ones masks) instead of branching per entry.  Measured slower (C2
-// probe 0.5145 vs 0.5004 ms, profiles/r02/s10/ab3_*): off.
-#ifndef PBF_GATHER_BRANCHFREE
-#define PBF_GATHER_BRANCHFREE 0
-#endif
 #ifndef PBF_GATHER_U
 #define PBF_GATHER_U 4
 #endif
 #ifndef PBF_GATHER_RFIRST_SORT
 #define PBF_GATHER_RFIRST_SORT 0
-#endif
-// PBF_HW_SLICES=1: gather splits write their words to their own slice of hw (k_hw_to_hitmask
-// ANDs the slices) instead of ANDing them into one word array with device-scope atomics.
-// Measured slower (C2 probe 0.504 vs 0.507 ms, C5 9.49 vs 9.61 ms: profiles/r02/s10/ab2_*): off.
-#ifndef PBF_HW_SLICES
-#define PBF_HW_SLICES 0
 #endif
 
 __device__ __forceinline__ uint4 ld_stream(const uint32_t* p) { return ld_stream_nt<PBF_NT_LOAD != 0>(p); }
@@ -662,8 +650,7 @@ __global__ void __launch_bounds__(1024) k_tile_probe_set(TileMap tm, PartGeom pg
 __global__ void __launch_bounds__(512) k_gather(TileMap tm, PartGeom pg, uint64_t n,
                                                 const uint32_t* __restrict__ regions, const uint32_t* __restrict__ R,
                                                 const uint32_t* __restrict__ subcnt, const uint32_t* __restrict__ neg,
-                                                uint8_t* __restrict__ hitmask, uint32_t* __restrict__ hw,
-                                                uint64_t hw_stride) {
+                                                uint8_t* __restrict__ hitmask, uint32_t* __restrict__ hw) {
     extern __shared__ uint32_t smem[];
     const uint32_t B = tm.nbuckets, cap = pg.cap, wpr = cap / 32, nsub = pg.nsub;
     const uint32_t tid = threadIdx.x, nt = blockDim.x;
@@ -778,11 +765,7 @@ __global__ void __launch_bounds__(512) k_gather(TileMap tm, PartGeom pg, uint64_
     }
     lds_barrier();
     if (S > 1) {  // this split's words into hw (k_hw_to_hitmask writes the hit mask)
-#if PBF_HW_SLICES
-        for (uint32_t w = tid; w * 32 < nkeys; w += nt) hw[sp * hw_stride + (k0 >> 5) + w] = kbits[w];
-#else
         for (uint32_t w = tid; w * 32 < nkeys; w += nt) atomicAnd(hw + (k0 >> 5) + w, kbits[w]);
-#endif
         return;
     }
     // hit-mask words for keys [k0, k1): k0 is a multiple of 64
@@ -797,15 +780,12 @@ __global__ void __launch_bounds__(512) k_gather(TileMap tm, PartGeom pg, uint64_
     }
 }
 
-// hw (gather words, one per 32 keys; S slices `stride` words apart, ANDed) → the LSB-first hit
-// mask of n keys.
-__global__ void k_hw_to_hitmask(const uint32_t* __restrict__ hw, uint64_t n, uint8_t* __restrict__ hitmask,
-                                uint32_t S, uint64_t stride) {
+// hw (ANDed gather words, one per 32 keys) → the LSB-first hit mask of n keys.
+__global__ void k_hw_to_hitmask(const uint32_t* __restrict__ hw, uint64_t n, uint8_t* __restrict__ hitmask) {
     const uint64_t nw = (n + 31) / 32;
     for (uint64_t w = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; w < nw; w += uint64_t(gridDim.x) * blockDim.x) {
         const uint64_t key0 = w * 32;
-        uint32_t bits = hw[w];
-        for (uint32_t q = 1; q < S; ++q) bits &= hw[q * stride + w];
+        const uint32_t bits = hw[w];
         const uint64_t nbt = min<uint64_t>(4, (n - key0 + 7) / 8);
         if (nbt == 4 && (reinterpret_cast<uintptr_t>(hitmask + key0 / 8) & 3) == 0)
             *reinterpret_cast<uint32_t*>(hitmask + key0 / 8) = bits;

@@ -56,7 +56,7 @@ int main(int argc, char** argv) {
             const size_t lg = size_t((pg.kpw + 31) / 32) * 4 + size_t(B) * (pg.nsub + 1) * 2 + 16;
             hipFuncSetAttribute((const void*)k_gather, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lg);
             hipEventRecord(c);
-            k_gather<<<dim3(pg.G, 1), 512, lg>>>(tm, pg, n, regions, R, subcnt, neg, hm, nullptr, 0);
+            k_gather<<<dim3(pg.G, 1), 512, lg>>>(tm, pg, n, regions, R, subcnt, neg, hm, nullptr);
             hipEventRecord(d); hipEventSynchronize(d); hipEventElapsedTime(&ms_gather, c, d);
             printf("k_tile_probe %.1f us, k_gather %.1f us (stamped)\n", ms_tile * 1e3, ms_gather * 1e3);
         }
