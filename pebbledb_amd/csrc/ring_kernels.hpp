@@ -35,6 +35,9 @@
 namespace pbf {
 
 constexpr uint32_t kRingKeysPerSub = 1024;  // = threads; slot field is 10 bits
+#ifndef PBF_RING_U24
+#define PBF_RING_U24 1
+#endif
 static_assert(kSlotShift == 20 && kRingKeysPerSub == 1024, "ring entry = (j & 3) << 30 | slot << 20 | position");
 // 2 measured best with the non-temporal streams (C2 A/B over 1/2/3/4/8: profiles/r01/s11/ab.txt)
 #ifndef PBF_RING_PREFETCH
@@ -106,7 +109,12 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
 #ifndef PBF_REGION_TILE_MAJOR
     // this workgroup's regions; an entry's offset in them fits 32 bits (B * cap < 2^32)
     uint32_t* const rgn = regions + uint64_t(g) * B * cap;
+#if PBF_RING_U24
+    // tb < 4096 and cap < 2^20 (plan_for): a 24-bit multiply-add (full rate), not a 64-bit mad
+    auto region_at = [&](uint32_t tb, uint32_t e) { return rgn + (__umul24(tb, cap) + e); };
+#else
     auto region_at = [&](uint32_t tb, uint32_t e) { return rgn + (tb * cap + e); };
+#endif
 #else
     auto region_at = [&](uint32_t tb, uint32_t e) { return regions + region_id(g, tb, pg.G, B) * cap + e; };
 #endif
