@@ -461,8 +461,7 @@ def sets_main(args, rank, world, local, torch, dist, np):
                          "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "kernel": pk,
                          "algorithmic_bytes": int(b_pass), "avg_ms": round(pass_ms, 4)},
             "check": {"members_all_hit": ok},
-            "rccl_world_size": dist.get_world_size() if world > 1 else 1,
-            "backend": (dist.get_backend() if world > 1 else None),
+            **dist_report(dist, world),
         }
         if fp_rate is not None:
             out["check"]["fp_rate_1M_absent"] = fp_rate
@@ -547,7 +546,7 @@ def sst_main(args, rank, world, local, torch, dist, np):
     f, metas, _ = build_sstable(hkeys, hvals)
     th = time.perf_counter() - th
     # the flush without list[str]: the memtable's encoded records (the
-    # values of memtable.map, Record.to_bytes) drained by the C packer into the boundary layout,
+    # memtable.map iterates them in key order, Record.to_bytes) drained by the C packer into the boundary layout,
     # then the same device SSTable build -> file bytes; checked byte-identical to the list path
     import struct
     from pebbledb_amd.keys import PackedRecords
@@ -638,6 +637,17 @@ def spawn_ranks(args) -> int:
     return rc
 
 
+def dist_report(dist, world):
+    """The process group the timing went over: its backend and the world size it saw.  The key
+    is rccl_world_size only when that backend is RCCL ("nccl" on ROCm); a gloo rehearsal reports
+    world_size_seen instead."""
+    if world == 1:
+        return {"backend": None, "world_size_seen": 1}
+    be = dist.get_backend()
+    key = "rccl_world_size" if be == "nccl" else "world_size_seen"
+    return {"backend": be, key: dist.get_world_size()}
+
+
 def dry_run(args, rank, world, dist):
     """Launcher and plumbing check without a GPU: gloo rendezvous on 127.0.0.1, the barrier
     and the max-over-ranks of the timed region as a real run does them.  Reports no number."""
@@ -690,14 +700,17 @@ def main():
     torch.cuda.set_device(local)
     if world > 1:
         # RCCL carries only the timing plumbing (barrier, max over ranks): the data path has no
-        # collective.  If it cannot start, the run goes on over gloo and says so.
+        # collective.  If RCCL cannot start the run fails (exit 3) rather than
+        # silently timing over another backend; gloo only when asked for (PBF_BENCH_BACKEND=gloo,
+        # the one-GPU rehearsal).
         backend = os.environ.get("PBF_BENCH_BACKEND", "nccl")
         if backend == "nccl":
             try:
                 dist.init_process_group(backend="nccl", init_method="env://", device_id=torch.device("cuda", local))
-            except Exception as e:  # noqa: BLE001 - reported, then the gloo rendezvous
-                print(f"rank {rank}: RCCL process group failed ({e!r}); timing plumbing over gloo", file=sys.stderr)
-                dist.init_process_group(backend="gloo", init_method="env://")
+            except Exception as e:  # noqa: BLE001 - reported, then a non-zero exit
+                print(f"rank {rank}: RCCL process group failed ({e!r}); set PBF_BENCH_BACKEND=gloo for a "
+                      f"gloo-timed rehearsal", file=sys.stderr)
+                sys.exit(3)
         else:
             dist.init_process_group(backend=backend, init_method="env://")
 
@@ -879,8 +892,7 @@ def main():
             "traffic_source": traffic["source"] if traffic else "no PMC summary for this library build",
             "check": {"members_all_hit": members_ok, "false_positives": fp, "probes_absent": n,
                       "fp_expected": round(fp_expect, 2), "fp_within_3x_expected": bool(fp_ok)},
-            "rccl_world_size": dist.get_world_size() if world > 1 else 1,
-            "backend": (dist.get_backend() if world > 1 else None),
+            **dist_report(dist, world),
         }
         if host_inc is not None:
             out["host_inclusive"] = host_inc

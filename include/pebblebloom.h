@@ -55,6 +55,7 @@ extern "C" {
 #define PBF_DETAIL_RING 1    /* tiled: ring partition (k_part_ring) */
 #define PBF_DETAIL_SORT 2    /* tiled: counting-sort partition (k_part) */
 #define PBF_DETAIL_ONE_KEY 4 /* pbf_may_contain's one-key launch */
+#define PBF_DETAIL_SET 8     /* multi-filter direct probe (k_probe_set: each key hashed once for the set) */
 
 typedef struct pbf_filter pbf_filter_t;
 
@@ -93,11 +94,15 @@ int pbf_probe(pbf_filter_t* f, const uint8_t* keys, const uint64_t* offsets, uin
  * (src/lsm_storage.py:164-169 L0 newest-first, :173-175 per level): hitmasks[i] receives
  * may_contain over the batch for filters[i], ceil(n/8) bytes LSB-first, host or device memory as
  * keys_on_device says (hitmasks itself is a host array of nfilters pointers).  All filters
- * must be on one device and distinct.  When they share (nb_bytes, k) -- one SSTable size class,
- * the usual case -- the keys are hashed and partitioned once for up to 8 filters and only the
- * tile test and gather run per filter; otherwise each filter is probed on its own stream.  With
- * keys_on_device = 1 the call is asynchronous on filters[0]'s stream (pbf_sync(filters[0]));
- * every other filter's stream is ordered before and after it. */
+ * must be on one device and distinct.  When they share (nb_bytes, k) and are large (the tiled
+ * probe) the keys are hashed and partitioned once for up to 8 filters and only the tile test
+ * and gather run per filter.  Otherwise -- SSTable filters of mixed sizes, the usual LSM case
+ * (each sized from its own key count, sstable.py:274) -- the filters whose own probe is direct
+ * are probed by one kernel per k and 64 filters that hashes every key ONCE and tests every
+ * filter from those hashes (MurmurHash3 does not depend on m); large filters of distinct sizes
+ * each run their own pipeline on their own stream.  With keys_on_device = 1 the call is
+ * asynchronous on filters[0]'s stream (pbf_sync(filters[0])); every other filter's stream is
+ * ordered before and after it. */
 int pbf_probe_multi_fixed(pbf_filter_t* const* filters, uint32_t nfilters, const uint8_t* keys, uint32_t key_len,
                           uint64_t n, uint8_t* const* hitmasks, int keys_on_device);
 int pbf_probe_multi(pbf_filter_t* const* filters, uint32_t nfilters, const uint8_t* keys, const uint64_t* offsets,
@@ -109,6 +114,15 @@ int pbf_probe_multi(pbf_filter_t* const* filters, uint32_t nfilters, const uint8
  * hit byte comes back the same way (one launch, no copies, no allocation after the first call
  * on a thread). */
 int pbf_may_contain(pbf_filter_t* f, const uint8_t* key, uint64_t len, int* out);
+
+/* LsmStorage.get's bloom checks for ONE key over a set of SSTable filters of any sizes
+ * (lsm_storage.py:164-179: every L0 filter, then each level filter whose key range holds the
+ * key — the range check stays with the caller): out_bits[i >> 3] bit (i & 7) =
+ * filters[i].may_contain(key), ceil(nfilters/8) bytes LSB-first.  One launch per k and 64
+ * filters (the key hashed once, one lane per filter), the key in and the answer out through
+ * mapped pinned memory; synchronous.  All filters on one device (a filter may repeat). */
+int pbf_may_contain_set(pbf_filter_t* const* filters, uint32_t nfilters, const uint8_t* key, uint64_t len,
+                        uint8_t* out_bits);
 
 /* mmh3.hash(key, seed) (bloom_filter.py:46: MurmurHash3_x86_32, signed int32) of one host key
  * of at most 4096 bytes, computed on `device` (one launch). */
@@ -149,8 +163,7 @@ int pbf_last_build_mode(pbf_filter_t* f);
 int pbf_set_probe_mode(pbf_filter_t* f, int mode);
 int pbf_last_probe_mode(pbf_filter_t* f);
 uint32_t pbf_last_probe_detail(pbf_filter_t* f);
-/* How the last tiled build ran: PBF_DETAIL_RING or _SORT | log2(tiles per super-tile) << 8 |
- * (keys per sub-chunk / 256) << 12. */
+/* How the last tiled build ran: PBF_DETAIL_RING or _SORT | (keys per sub-chunk / 256) << 12. */
 uint32_t pbf_last_build_detail(pbf_filter_t* f);
 
 /* Release the device's pooled working memory (waits for its last users); the next call

@@ -3,7 +3,7 @@
 Drop-in for MaudGautier/pebbledb ``src/bloom_filter.py`` (``BloomFilter``), backed by
 hand-written HIP kernels for gfx950 in ``libpebblebloom.so`` (C-ABI: include/pebblebloom.h).
 """
-from .bloom_filter import BloomFilter, may_contain_multi, probe_multi_device, set_default_device
+from .bloom_filter import BloomFilter, may_contain_multi, may_contain_set, probe_multi_device, set_default_device
 from .keys import PackedKeys
 
-__all__ = ["BloomFilter", "PackedKeys", "may_contain_multi", "probe_multi_device", "set_default_device"]
+__all__ = ["BloomFilter", "PackedKeys", "may_contain_multi", "may_contain_set", "probe_multi_device", "set_default_device"]

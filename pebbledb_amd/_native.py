@@ -19,7 +19,7 @@ PBF_ERR_HIP = -2
 PBF_ERR_ZERO_SIZE = -3
 PBF_BUILD_AUTO, PBF_BUILD_ATOMIC, PBF_BUILD_TILED = 0, 1, 2
 PBF_PROBE_AUTO, PBF_PROBE_DIRECT, PBF_PROBE_TILED = 0, 1, 2
-PBF_DETAIL_RING, PBF_DETAIL_SORT, PBF_DETAIL_ONE_KEY = 1, 2, 4
+PBF_DETAIL_RING, PBF_DETAIL_SORT, PBF_DETAIL_ONE_KEY, PBF_DETAIL_SET = 1, 2, 4, 8
 
 _u8p = ctypes.c_void_p
 _vp = ctypes.c_void_p
@@ -57,6 +57,7 @@ SIGNATURES = {
     "pbf_last_probe_detail": (_u32, [_vp]),
     "pbf_last_build_detail": (_u32, [_vp]),
     "pbf_may_contain": (_int, [_vp, ctypes.c_char_p, _u64, ctypes.POINTER(_int)]),
+    "pbf_may_contain_set": (_int, [_vp, _u32, ctypes.c_char_p, _u64, _u8p]),
     "pbf_trim": (_int, [_int]),
     "pbf_scratch_bytes": (_int, [_int, ctypes.POINTER(_u64)]),
     "pbf_encode_data_blocks": (_int, [_int, _u8p, _vp, _u8p, _vp, _u64, _vp, _vp, _u64, _u8p, _int]),

@@ -59,6 +59,10 @@ class BloomFilter:
         self._pending: list[str] = []
         self._plock = threading.Lock()  # guards _pending (add / flush from several threads)
         self._h = None
+        # the part of a `bits` int outside the bitmap (bits >= 8*nb_bytes, or a negative int's
+        # sign extension): the reference keeps the whole int (bloom_filter.py:31) and compares it
+        # in __eq__ (:36), while only the low 8*nb_bytes bits are ever read or serialised
+        self._extra = 0
         if nb_bytes > 0:
             h = ctypes.c_void_p()
             _native.check(_native.lib().pbf_create(self.device, nb_bytes, nb_hash_functions, ctypes.byref(h)),
@@ -86,13 +90,15 @@ class BloomFilter:
 
     def _upload_int(self, bits: int) -> None:
         """The reference stores any int as ``bits`` and only ever reads its low 8*nb_bytes bits
-        (``to_bytes`` bloom_filter.py:78 and ``_is_bit_set`` with indices < bits_size): bits
-        outside that range (and a negative int's infinite sign extension) are dropped here."""
-        if self.nb_bytes <= 0:
-            raise ValueError("bits given for a filter with nb_bytes <= 0")
-        masked = int(bits) & ((1 << (8 * self.nb_bytes)) - 1)
-        data = np.frombuffer(masked.to_bytes(self.nb_bytes, "little"), dtype=np.uint8)
-        _native.check(_native.lib().pbf_set_bitmap(self._h, _vp(data), self.nb_bytes), "pbf_set_bitmap")
+        (``to_bytes`` bloom_filter.py:78 and ``_is_bit_set`` with indices < bits_size): those go to
+        the device bitmap; the rest of the int (bits outside that range, a negative int's sign
+        extension) is kept on the host for ``bits`` and ``__eq__``."""
+        bits = int(bits)
+        low = bits & ((1 << (8 * self.nb_bytes)) - 1) if self.nb_bytes > 0 else 0
+        self._extra = bits - low
+        if self.nb_bytes > 0:
+            data = np.frombuffer(low.to_bytes(self.nb_bytes, "little"), dtype=np.uint8)
+            _native.check(_native.lib().pbf_set_bitmap(self._h, _vp(data), self.nb_bytes), "pbf_set_bitmap")
 
     def _flush(self) -> None:
         if self._pending:
@@ -142,16 +148,17 @@ class BloomFilter:
     @property
     def bits(self) -> int:
         """The filter as one Python int (bloom_filter.py:31), materialised on demand."""
-        return int.from_bytes(self.bitmap(), "little")
+        return int.from_bytes(self.bitmap(), "little") + self._extra
 
     @bits.setter
     def bits(self, value: int) -> None:
         with self._plock:
             self._pending = []
+        self._extra = 0
         if self.nb_bytes > 0:
             _native.check(_native.lib().pbf_clear(self._h), "pbf_clear")
-            if value:
-                self._upload_int(value)
+        if value:
+            self._upload_int(value)
 
     def __eq__(self, other):
         # bloom_filter.py:33-36 — compares bits and k only (not nb_bytes)
@@ -159,6 +166,8 @@ class BloomFilter:
             return NotImplemented
         if self.nb_hash_functions != other.nb_hash_functions:
             return False
+        if self._extra or other._extra:
+            return self.bits == other.bits
         return self.bitmap().rstrip(b"\0") == other.bitmap().rstrip(b"\0")
 
     __hash__ = None
@@ -321,7 +330,7 @@ class BloomFilter:
 
     @property
     def last_build_detail(self) -> int:
-        """PBF_DETAIL_RING/SORT | log2(tiles per super-tile) << 8 | (keys per sub-chunk / 256) << 12."""
+        """PBF_DETAIL_RING/SORT | (keys per sub-chunk / 256) << 12."""
         return 0 if self._h is None else int(_native.lib().pbf_last_build_detail(self._h))
 
     @property
@@ -386,6 +395,27 @@ def may_contain_multi(filters, keys) -> np.ndarray:
             rc = L.pbf_probe_multi(hs, len(native), _vp(pk.data), _vp(pk.offsets), pk.n, outs, 0)
         _native.check(rc, "pbf_probe_multi")
     return out
+
+
+def may_contain_set(filters, key: str) -> list[bool]:
+    """``filters[i].may_contain(key)`` for every filter, in ONE launch per k (pbf_may_contain_set):
+    the per-key form of LsmStorage.get's bloom checks over its L0 and in-range level SSTables
+    (src/lsm_storage.py:164-179).  Filters may have any sizes; they must share a device."""
+    filters = list(filters)
+    if not filters:
+        return []
+    native = _native_set(filters)
+    res = [True] * len(filters)  # k == 0: the AND over no bits
+    if native:
+        enc = key.encode("utf-8")
+        hs = (ctypes.c_void_p * len(native))(*[filters[i]._h.value for i in native])
+        out = np.zeros((len(native) + 7) // 8, dtype=np.uint8)
+        _native.check(_native.lib().pbf_may_contain_set(hs, len(native), enc, len(enc), _vp(out)),
+                      "pbf_may_contain_set")
+        bits = np.unpackbits(out, bitorder="little")
+        for j, i in enumerate(native):
+            res[i] = bool(bits[j])
+    return res
 
 
 def probe_multi_device(filters, keys_ptr: int, n: int, hitmask_ptrs, key_len: int = 0, offsets_ptr: int = 0) -> None:

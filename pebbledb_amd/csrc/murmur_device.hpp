@@ -69,42 +69,9 @@ __device__ __forceinline__ uint32_t load_tail(const uint8_t* p, uint32_t t) {
     return v & ((1u << (8 * t)) - 1u);
 }
 
-// k seeds of MurmurHash3_x86_32 for one key, sbase .. sbase+k-1; emit(s, hash_u32) is called
-// for s = 0..k-1 (seed sbase + s).  KMAX is the compile-time register budget for seed states
-// (k <= KMAX).
-template <int KMAX, class Emit>
-__device__ __forceinline__ void murmur_seeds(const uint8_t* p, uint32_t len, int k, Emit&& emit, int sbase = 0) {
-    uint32_t h[KMAX];
-#pragma unroll
-    for (int s = 0; s < KMAX; ++s) h[s] = uint32_t(sbase + s);
-    const uint32_t nb = len >> 2;
-    const bool aligned = (reinterpret_cast<uintptr_t>(p) & 3) == 0;
-    if (aligned) {
-        const uint32_t* q = reinterpret_cast<const uint32_t*>(p);
-        for (uint32_t b = 0; b < nb; ++b) {
-            const uint32_t km = mix_block(q[b]);
-#pragma unroll
-            for (int s = 0; s < KMAX; ++s) h[s] = round_h(h[s], km);
-        }
-    } else {
-        for (uint32_t b = 0; b < nb; ++b) {
-            const uint32_t km = mix_block(load_u32_any(p + 4 * b));
-#pragma unroll
-            for (int s = 0; s < KMAX; ++s) h[s] = round_h(h[s], km);
-        }
-    }
-    const uint32_t t = len & 3;
-    if (t) {
-        const uint32_t km = mix_block(load_tail(p + 4 * nb, t));
-#pragma unroll
-        for (int s = 0; s < KMAX; ++s) h[s] ^= km;
-    }
-#pragma unroll
-    for (int s = 0; s < KMAX; ++s)
-        if (s < k) emit(s, fmix32(h[s] ^ len));
-}
-
-// Same hashes for a key at any byte address, read as aligned 16-byte chunks (4 dwordx4 loads in
+// k seeds of MurmurHash3_x86_32 for one key at any byte address, sbase .. sbase+k-1; emit(s,
+// hash_u32) is called for s = 0..k-1 (seed sbase + s).  KMAX is the compile-time register budget
+// for seed states (k <= KMAX).  The key is read as aligned 16-byte chunks (4 dwordx4 loads in
 // flight per 64 bytes) instead of two dword loads per 4-byte block.  Every chunk read holds at
 // least one byte of the key (first chunk = floor16(p), last = the one holding p[len-1]), so the
 // reads never leave a page the key touches.  Block j = bytes p[4j, 4j+4) = alignbyte(W[w0+j+1],

@@ -29,6 +29,7 @@
 #include "ring_kernels.hpp"
 #include "sstable_kernels.hpp"
 #include "lsm_kernels.hpp"
+#include "set_kernels.hpp"
 
 using namespace pbf;
 
@@ -49,6 +50,14 @@ int fail(int code, const std::string& msg) {
     } while (0)
 
 #define CHECK_LAUNCH() HIP_TRY(hipGetLastError())
+// after a launch on f's stream: checks it and names it as the stream's last kernel (reported by
+// wait_stream when the stream does not finish in time)
+#define LAUNCHED(f, name)           \
+    do {                            \
+        (f)->last_kernel = (name);  \
+        (f)->pending = true;        \
+        CHECK_LAUNCH();             \
+    } while (0)
 
 struct DevBuf {
     void* p = nullptr;
@@ -107,52 +116,9 @@ size_t stage_bytes() {
 }
 constexpr uint64_t kMaxPositions = uint64_t(1) << 30; // tiled pipeline batch (4 GiB of positions)
 
-// Rounds of the ring-partition tiled probe (PBF_PROBE_ROUNDS=2 selects two; default one: the
-// second round still pays the partition's per-sub-chunk cost for every key, measured slower).
-int probe_rounds() {
-    static const int v = [] {
-        const char* e = std::getenv("PBF_PROBE_ROUNDS");
-        const int x = e ? std::atoi(e) : 0;
-        return x > 0 ? x : 1;
-    }();
-    return v;
-}
-
-// Keys per tiled-probe pipeline (PBF_PROBE_CHUNK overrides; 0 = as large as the plan allows).
-// Smaller pipelines keep one pipeline's region entries plus the bitmap inside the 256 MiB
-// Infinity Cache between the partition's writes and the tile test's / gather's reads.
-uint64_t probe_chunk() {
-    static const uint64_t v = [] {
-        const char* e = std::getenv("PBF_PROBE_CHUNK");
-        const long long x = e ? std::atoll(e) : 0;
-        return x > 0 ? (uint64_t(x) + 63) & ~uint64_t(63) : uint64_t(0);
-    }();
-    return v;
-}
-
-// Overlapped probe pipelines (PBF_PROBE_OVERLAP = chunk count >= 2; 0/1 = one pipeline): the
-// batch is cut into chunks whose pipelines alternate between the filter's stream and a side
-// stream, each with its own scratch set; chunk c's partition (instruction-bound) starts when
-// chunk c-1's partition is done, so it runs beside chunk c-1's tile test and gather
-// (memory-bound).
-uint32_t probe_overlap() {
-    static const uint32_t v = [] {
-        const char* e = std::getenv("PBF_PROBE_OVERLAP");
-        const int x = e ? std::atoi(e) : 0;
-        return x >= 2 ? uint32_t(std::min(x, 16)) : 0u;
-    }();
-    return v;
-}
-
-// Words loaded in the probe's first stage (PBF_PROBE_S1 overrides; tuning knob).
-int probe_stage1() {
-    static const int v = [] {
-        const char* e = std::getenv("PBF_PROBE_S1");
-        const int x = e ? std::atoi(e) : 0;
-        return x > 0 ? x : 2;
-    }();
-    return v;
-}
+// Words loaded in the direct probe's first stage (k_probe): 2 measured best of 1/2/6
+// (profiles/r02/s1, the direct probe is the small-batch path).
+constexpr int kProbeStage1 = 2;
 
 // Most partition workgroups of one pipeline (PBF_PART_G overrides; default 256 = one per CU).
 // More workgroups mean fewer keys each: smaller gather key bitmaps and run tables.
@@ -259,7 +225,7 @@ namespace {
 // one for the duration of its host-side enqueue, and the GPU-side reuse across streams is
 // ordered by the set's `last` event (the next user's stream waits on it).
 struct Scratch {
-    DevBuf regions, fill, ovf, ovf_count, subcnt, rbits, neg, alive, hw;
+    DevBuf regions, fill, ovf, ovf_count, subcnt, rbits, neg, hw;
     uint32_t ovf_phase = 0;  // which of the two overflow counters the next build uses
     bool ovf_init = false;
     DevBuf dkeys, doffs, dout;
@@ -270,7 +236,7 @@ struct Scratch {
     hipStream_t last_stream = nullptr;  // ... on this stream
     bool leased = false;
     void release_all() {
-        for (DevBuf* d : {&regions, &fill, &ovf, &ovf_count, &subcnt, &rbits, &neg, &alive, &hw, &dkeys, &doffs, &dout,
+        for (DevBuf* d : {&regions, &fill, &ovf, &ovf_count, &subcnt, &rbits, &neg, &hw, &dkeys, &doffs, &dout,
                           &svals, &splan, &ssec, &serr})
             d->release();
         pin[0].release();
@@ -323,12 +289,12 @@ struct pbf_filter {
     int probe_mode = PBF_PROBE_AUTO;
     int last_probe_mode = 0;
     uint32_t last_probe_detail = 0;  // PBF_DETAIL_* of the last probe
-    uint32_t last_build_detail = 0;  // PBF_DETAIL_* | sb << 8 | (kps / 256) << 12 of the last tiled build
+    uint32_t last_build_detail = 0;  // PBF_DETAIL_* | (kps / 256) << 12 of the last tiled build
     Scratch* sc = nullptr;           // leased for the current call
     uint64_t* dpop = nullptr;
     hipEvent_t ev = nullptr;       // stream joins of multi-filter probes
-    hipEvent_t ev_part = nullptr;  // overlapped probe chunks: partition done / side stream joins
-    hipEvent_t ev_side = nullptr;
+    const char* last_kernel = "";  // the last kernel enqueued on the stream (wait_stream's report)
+    bool pending = false;          // work may be queued on the stream since its last completed wait
     std::mutex mu;                 // one host thread inside the handle at a time
 };
 
@@ -485,64 +451,10 @@ hipError_t pooled_stream(int device, hipStream_t* out) {
     return hipSuccess;
 }
 
-// One extra stream per device for the overlapped probe chunks (created on first use).
-hipError_t side_stream(int device, hipStream_t* out) {
-    static std::mutex mu;
-    static std::map<int, hipStream_t> side;
-    std::lock_guard<std::mutex> lock(mu);
-    auto it = side.find(device);
-    if (it == side.end()) {
-        hipStream_t st = nullptr;
-        const hipError_t e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
-        if (e != hipSuccess) return e;
-        it = side.emplace(device, st).first;
-    }
-    *out = it->second;
-    return hipSuccess;
-}
-
 // Lease a scratch set of f's device for work enqueued on f's stream (RAII).  Prefers a set
 // whose previous work is done or was on this same stream; creates one while fewer than
 // max_scratch_sets() exist; otherwise takes a free set and orders this stream after its
 // previous user.
-Scratch* pick_set(int device, hipStream_t st) {
-    DevicePool& pool = device_pool(device);
-    std::lock_guard<std::mutex> lock(pool.mu);
-    Scratch* any = nullptr;
-    for (Scratch* s : pool.sets) {
-        if (s->leased) continue;
-        if (!any) any = s;
-        if (!s->last || s->last_stream == st || event_done(s->last)) {
-            s->leased = true;
-            return s;
-        }
-    }
-    Scratch* pick = nullptr;
-    if (pool.sets.size() < max_scratch_sets() || !any) {
-        pick = new Scratch();
-        pool.sets.push_back(pick);
-    }
-    if (!pick) pick = any;
-    pick->leased = true;
-    return pick;
-}
-
-// A second set for work on another stream `st` (released with return_set on that stream).
-int lease_set(int device, hipStream_t st, Scratch** out) {
-    Scratch* s = pick_set(device, st);
-    *out = s;
-    if (!s->last) HIP_TRY(hipEventCreateWithFlags(&s->last, hipEventDisableTiming));
-    if (s->last_stream && s->last_stream != st) HIP_TRY(hipStreamWaitEvent(st, s->last, 0));
-    return PBF_OK;
-}
-
-void return_set(int device, Scratch* s, hipStream_t st) {
-    if (hipEventRecord(s->last, st) == hipSuccess) s->last_stream = st;
-    DevicePool& pool = device_pool(device);
-    std::lock_guard<std::mutex> lock(pool.mu);
-    s->leased = false;
-}
-
 class Lease {
    public:
     Lease(pbf_filter_t* f) : f_(f) {}
@@ -598,6 +510,7 @@ class Lease {
 // Bring a pristine bitmap to its explicit all-zero form (before atomics / reads).
 int materialise(pbf_filter_t* f) {
     if (!f->pristine) return PBF_OK;
+    f->pending = true;
     HIP_TRY(hipMemsetAsync(f->bitmap, 0, f->alloc_words * 4, f->stream));
     f->pristine = false;
     return PBF_OK;
@@ -625,6 +538,17 @@ Batch make_batch(const uint8_t* keys, const uint64_t* offsets, uint32_t key_len,
     return b;
 }
 
+// Keys [i0, i0 + n) of a batch (offsets stay relative to off0, so a slice needs no rebasing).
+Batch slice(const Batch& b, uint64_t i0, uint64_t n) {
+    Batch c = b;
+    c.n = n;
+    if (b.km == kVar)
+        c.ks.offsets = b.ks.offsets + i0;
+    else
+        c.ks.data = b.ks.data + i0 * b.ks.key_len;
+    return c;
+}
+
 uint32_t grid_for(uint64_t n, uint32_t block, uint32_t cap = 16384) {
     uint64_t g = (n + block - 1) / block;
     return uint32_t(std::max<uint64_t>(1, std::min<uint64_t>(g, cap)));
@@ -638,7 +562,7 @@ int run_atomic(pbf_filter_t* f, const Batch& b) {
         k_build_atomic<decltype(KMAX)::value, decltype(KM)::value>
             <<<grid, 256, 0, f->stream>>>(b.ks, b.n, int(f->k), f->im, f->bitmap);
     });
-    CHECK_LAUNCH();
+    LAUNCHED(f, "k_build_atomic");
     return PBF_OK;
 }
 
@@ -664,57 +588,22 @@ int part_override() {
 }
 
 // Ring partition (ring_kernels.hpp) when there are many tiles: a 1024-key sub-chunk then puts
-// only a few positions into each tile (<= GS/2 on average), which is what the ring's GS-entry
+// only a few positions into each tile (<= GS/2 = 8 on average), which is what the ring's 16-entry
 // groups need, while the counting-sort partition's per-tile runs get too short to write well.
-// Ring of 32 entries (64-B groups) up to 1024 tiles, of 16 (32-B groups) up to 2048.
+// The 32-entry rings of B tiles take B * 128 B of LDS: up to 1024 tiles.  (Rings for more tiles
+// — super-tiles of 2^sb tiles, or 16-entry rings — measured slower than the counting sort for
+// C3 / C4 and were removed: profiles/r02/s2, profiles/r02/s9.)
 bool ring_pow2(const TileMap& tm) { return tm.im.mode == kPow2 && !tm.cspace; }
 
-uint32_t ring_entries(uint32_t B, uint32_t k, bool probe, uint32_t tb) {
-    if ((probe && tb > kSlotShift) || k > 16) return 0;
+// Keys per sub-chunk of a ring partition of B tiles and k hashes (0 = the ring does not apply):
+// the largest of 1024 / 512 / 256 with kps * k <= B * GS / 2.  Probes keep 1024 (the entry's
+// slot field), builds may take smaller sub-chunks (k = 10 over 1024 tiles: 512).
+uint32_t ring_kps(uint32_t B, uint32_t k, bool probe, uint32_t tb) {
     const int ov = part_override();
-    if (ov == 1) return 0;
-    const uint32_t rc = B <= 1024 ? 32 : (B <= 2048 ? 16 : 0);
-    if (!rc) return 0;
-    if (ov == 2) return rc;
-    // mean positions per tile per sub-chunk = 1024*k/B <= GS/2 = rc/4
-    return uint64_t(kRingKeysPerSub) * k * 4 <= uint64_t(B) * rc ? rc : 0;
-}
-
-// Ring BUILD geometry for any tile count: rings of 32 entries (64-B groups) per super-tile of
-// 2^sb tiles, with nsup = ceil(B / 2^sb) <= 1024 super-tiles (128 KiB of rings), and a sub-chunk
-// of kps keys small enough that a super-tile receives <= GS/2 = 8 positions per sub-chunk on
-// average.  C2 (B = 1024, k = 6): sb 0, kps 1024 (unchanged); C3 (B = 4096, k = 8): sb 2, kps
-// 1024; C4 (B = 1714, k = 10): sb 1, kps 512.  Returns false when no geometry fits.
-//
-// Measured (profiles/r02/s2): super-tiles lose.  C3 (sb 2): ring partition 4.05 ms vs the
-// counting-sort partition's 5.11, but the 4 sibling tile builders do not find each other's
-// region lines in L2 and read them 4x (2.20 ms vs 0.80); C4 (sb 1, kps 512): both kernels slower
-// (5.03 + 5.44 vs 3.80 + 4.14 ms per 107M-key pipeline).  So sb > 0 is opt-in (PBF_RING_SUPER=1)
-// and only sb = 0 geometries (<= 1024 tiles) take the ring build by default.
-bool ring_super_on() {
-    static const bool v = [] {
-        const char* e = std::getenv("PBF_RING_SUPER");
-        return e && std::atoi(e) != 0;
-    }();
-    return v;
-}
-
-bool ring_build_geometry(uint32_t B, uint32_t k, uint32_t* sb, uint32_t* nsup, uint32_t* kps) {
-    const int ov = part_override();
-    if (ov == 1 || k > 16 || k == 0) return false;
-    uint32_t s = 0;
-    while (((B + (1u << s) - 1) >> s) > 1024) ++s;
-    if (s > 3 || (s > 0 && !ring_super_on())) return false;
-    const uint32_t ns = (B + (1u << s) - 1) >> s;
-    for (uint32_t kp = 1024; kp >= 256; kp /= 2) {
-        if (uint64_t(kp) * k * 4 <= uint64_t(ns) * 32 || (ov == 2 && kp == 256)) {
-            *sb = s;
-            *nsup = ns;
-            *kps = kp;
-            return true;
-        }
-    }
-    return false;
+    if (ov == 1 || k == 0 || k > 16 || B > 1024 || (probe && tb > kSlotShift)) return 0;
+    for (uint32_t kp = kRingKeysPerSub; kp >= (probe ? kRingKeysPerSub : 256u); kp /= 2)
+        if (uint64_t(kp) * k * 4 <= uint64_t(B) * kRingEntries) return kp;
+    return ov == 2 ? (probe ? kRingKeysPerSub : 256u) : 0u;
 }
 
 // Gather LDS = the key bitmap of a partition workgroup + one u16 run-boundary row (`row`
@@ -729,12 +618,9 @@ void set_gather(PartPlan& pl, uint32_t B, uint32_t row, uint32_t nf = 1) {
     pl.lds_gather = lds(S);
     pl.gtq = 0;
     // the ring gather's quad table, when groups fit a byte and the workgroup stays small enough
-    // for 4 per CU (PBF_GATHER_QTAB=0 turns it off)
-    static const bool qtab_on = [] {
-        const char* e = std::getenv("PBF_GATHER_QTAB");
-        return !(e && std::atoi(e) == 0);
-    }();
-    if (qtab_on && pl.pg.ring && row <= 255) {
+    // for 4 per CU (measured neutral against the binary search, kept for the shorter path:
+    // profiles/r02/s3/gsweep_*)
+    if (pl.pg.ring && row <= 255) {
         const uint32_t tq = pl.pg.cap / 4;
         const size_t with = ((pl.lds_gather + 3) & ~size_t(3)) + size_t((B + S - 1) / S) * tq + 4;
         if (with <= 38 * 1024) {
@@ -742,42 +628,23 @@ void set_gather(PartPlan& pl, uint32_t B, uint32_t row, uint32_t nf = 1) {
             pl.lds_gather = with;
         }
     }
-    // the packed-quad loop's region prefix rq[nb + 1] (ring gather)
-    if (pl.pg.ring) pl.lds_gather = ((pl.lds_gather + 3) & ~size_t(3)) + (size_t((B + S - 1) / S) + 1) * 4 + 8;
 }
 
-// PBF_GATHER_PACKED=1: the ring gather walks its regions as one packed list of quads instead
-// of region by region.  Measured (profiles/r02/s6): C2 probe 0.619 vs 0.581 ms, C5 11.11 vs
-// 11.22 ms — so off by default.
-int gather_packed() {
-    static const int v = [] {
-        const char* e = std::getenv("PBF_GATHER_PACKED");
-        return (e && std::atoi(e) == 1) ? 1 : 0;
-    }();
-    return v;
-}
-
-PartPlan plan_ring(uint32_t B, uint32_t k, uint64_t n, uint32_t rc, double share, uint32_t nf = 1,
-                   uint32_t sb = 0, uint32_t kps_ = kRingKeysPerSub) {
+PartPlan plan_ring(uint32_t B, uint32_t k, uint64_t n, uint32_t kps, double share, uint32_t nf = 1) {
     PartPlan pl{};
-    const uint64_t kps = kps_;
-    const uint32_t nsup = (B + (1u << sb) - 1) >> sb;
-    share = std::min(1.0, share * double(1u << sb));  // a super-tile holds 2^sb tiles
-    pl.pg.sb = sb;
-    pl.pg.nsup = nsup;
     const uint64_t G0 = std::min<uint64_t>(part_max_groups(false), std::max<uint64_t>(1, (n + kps - 1) / kps));
     uint64_t kpw = (n + G0 - 1) / G0;
     kpw = ((kpw + kps - 1) / kps) * kps;
     pl.pg.G = uint32_t(std::max<uint64_t>(1, (n + kpw - 1) / kpw));
-    pl.pg.kps = uint32_t(kps);
+    pl.pg.kps = kps;
     pl.pg.kpw = kpw;
     pl.pg.nsub = uint32_t(kpw / kps);
     pl.pg.nq = (pl.pg.nsub + 3) / 4;
-    pl.pg.ring = rc;
+    pl.pg.ring = kRingEntries;
     const double mu = double(kpw) * k * share;
     const uint64_t cap = uint64_t(mu + 8.0 * std::sqrt(mu) + 32.0);
     pl.pg.cap = uint32_t(((cap + 31) / 32) * 32);
-    pl.lds_part = size_t((2 * nsup + 16 * 128 + 3) & ~3u) * 4 + size_t(nsup) * rc * 4;
+    pl.lds_part = size_t(ring_lds_words(B)) * 4;
     set_gather(pl, B, pl.pg.nq + 1, nf);
     return pl;
 }
@@ -806,7 +673,6 @@ PartPlan plan_partition(uint32_t B, uint32_t k, int km, uint64_t n, bool probe, 
     pl.pg.kps = uint32_t(kps);
     pl.pg.kpw = kpw;
     pl.pg.nsub = uint32_t(kpw / kps);
-    pl.pg.nsup = B;
     const double mu = double(kpw) * k * share;
     const uint64_t cap = uint64_t(mu + 8.0 * std::sqrt(mu) + 32.0);
     pl.pg.cap = uint32_t(((cap + 31) / 32) * 32);
@@ -839,44 +705,33 @@ double busiest_tile_share(const TileMap& tm) {
 PartPlan plan_for(const TileMap& tm, uint32_t k, int km, uint64_t n, bool probe, uint32_t nf = 1) {
     const uint32_t B = tm.nbuckets;
     const double share = busiest_tile_share(tm);
-    uint32_t sb, nsup, kps;
-    if (!probe && ring_build_geometry(B, k, &sb, &nsup, &kps)) {
-        const PartPlan pl = plan_ring(B, k, n, 32, share, 1, sb, kps);
-        // flush descriptors hold a region position in 20 bits; entry offsets within a
-        // workgroup's regions are 32-bit (nsup * cap < 2^32)
-        if (pl.pg.cap < (1u << 20) && uint64_t(pl.pg.nsup) * pl.pg.cap < (uint64_t(1) << 32)) return pl;
-    }
-    const uint32_t rc = probe ? ring_entries(B, k, probe, tm.tb) : 0;
-    if (rc) {
-        const PartPlan pl = plan_ring(B, k, n, rc, share, nf);
-        if (pl.pg.cap < (1u << 20) && uint64_t(pl.pg.nsup) * pl.pg.cap < (uint64_t(1) << 32)) return pl;
+    if (const uint32_t kps = ring_kps(B, k, probe, tm.tb)) {
+        const PartPlan pl = plan_ring(B, k, n, kps, share, probe ? nf : 1);
+        // head / tail are 16-bit halves in LDS (cap <= 32768); entry offsets within a
+        // workgroup's regions are 32-bit (B * cap < 2^32)
+        if (pl.pg.cap <= 32768 && uint64_t(B) * pl.pg.cap < (uint64_t(1) << 32)) return pl;
     }
     return plan_partition(B, k, km, n, probe, share);
 }
 
-// The ring partition kernel for (k, key layout, ring size): with the seed count and the 32-entry
-// ring fixed at compile time where it pays (k equal to the register bucket, or k = 6 — C2/C5's
-// k), its k LDS atomics per key issue back to back and its ring / flush arithmetic is shifts;
-// other k or ring sizes take the runtime kernel of their bucket.
+// The ring partition kernel for (k, key layout): with the seed count fixed at compile time
+// where it pays (k equal to the register bucket, or k = 6 — C2/C5's k), its k LDS atomics per
+// key issue back to back; other k take the runtime-k kernel of their bucket.
 template <int KX, int KMD, bool PROBE, class L>
-void with_ring_kernel(uint32_t k, uint32_t ring, uint32_t cap, bool pow2, L&& launch) {
+void with_ring_kernel(uint32_t k, bool pow2, L&& launch) {
     if constexpr (KMD != kFixedN) {
-        if (ring == 32 && cap <= 32768) {  // these kernels keep head / tail in 16 bits
-            if constexpr (KX == 8) {
-                if (k == 6) {
-                    launch(pow2 ? k_part_ring<6, KMD, PROBE, true, true, 32>
-                                : k_part_ring<6, KMD, PROBE, false, true, 32>);
-                    return;
-                }
-            }
-            if (k == uint32_t(KX)) {
-                launch(pow2 ? k_part_ring<KX, KMD, PROBE, true, true, 32>
-                            : k_part_ring<KX, KMD, PROBE, false, true, 32>);
+        if constexpr (KX == 8) {
+            if (k == 6) {
+                launch(pow2 ? k_part_ring<6, KMD, PROBE, true, true> : k_part_ring<6, KMD, PROBE, false, true>);
                 return;
             }
         }
+        if (k == uint32_t(KX)) {
+            launch(pow2 ? k_part_ring<KX, KMD, PROBE, true, true> : k_part_ring<KX, KMD, PROBE, false, true>);
+            return;
+        }
     }
-    launch(pow2 ? k_part_ring<KX, KMD, PROBE, true> : k_part_ring<KX, KMD, PROBE, false>);
+    launch(pow2 ? k_part_ring<KX, KMD, PROBE, true, false> : k_part_ring<KX, KMD, PROBE, false, false>);
 }
 
 // The counting-sort partition kernel for (k, key layout): exact-k variants for the k the
@@ -901,8 +756,8 @@ int run_tiled(pbf_filter_t* f, const Batch& b) {
     const uint32_t k = f->k;
     const PartPlan pl = plan_for(tm, k, b.km, b.n, false);
     const PartGeom& pg = pl.pg;
-    HIP_TRY(f->sc->regions.ensure(size_t(pg.G) * pg.nsup * pg.cap * 4));
-    HIP_TRY(f->sc->fill.ensure(size_t(pg.G) * pg.nsup * 4));
+    HIP_TRY(f->sc->regions.ensure(size_t(pg.G) * B * pg.cap * 4));
+    HIP_TRY(f->sc->fill.ensure(size_t(pg.G) * B * 4));
     HIP_TRY(f->sc->ovf.ensure(std::max<uint64_t>(b.n * k, 1) * 4));
     HIP_TRY(f->sc->ovf_count.ensure(64));
     if (!f->sc->ovf_init) {  // two counters, used alternately; each build's k_ovf_build zeroes the other
@@ -922,12 +777,11 @@ int run_tiled(pbf_filter_t* f, const Batch& b) {
             constexpr int KX = decltype(KMAX)::value, KMD = decltype(KM)::value;
             if (pg.ring) {
                 if constexpr (KX <= 16) {
-                    with_ring_kernel<KX, KMD, false>(k, pg.ring, pg.cap, ring_pow2(tm), [&](auto kern) {
+                    with_ring_kernel<KX, KMD, false>(k, ring_pow2(tm), [&](auto kern) {
                         err = allow_lds(kern, pl.lds_part);
                         if (err == hipSuccess)
                             kern<<<pg.G, kPartThreads, pl.lds_part, s>>>(b.ks, b.n, int(k), tm, pg, regions, fill,
-                                                                 nullptr, ovf, ovf_count, ProbeSet{}, 0, nullptr,
-                                                                 nullptr);
+                                                                 nullptr, ovf, ovf_count, ProbeSet{}, nullptr);
                     });
                 }
             } else {
@@ -941,34 +795,25 @@ int run_tiled(pbf_filter_t* f, const Batch& b) {
         }
     });
     HIP_TRY(err);
-    CHECK_LAUNCH();
+    LAUNCHED(f, pg.ring ? "k_part_ring<build>" : "k_part<build>");
     const size_t lds_tile = ((size_t(1) << tm.tb) / 32 + pg.G) * 4;
-    if (pg.ring && pg.sb > 0) {
-        HIP_TRY(allow_lds(k_tile_build<true>, lds_tile));
-        const uint32_t grid = ((pg.nsup + 7) / 8) * 8 * (1u << pg.sb);
-        k_tile_build<true><<<grid, 1024, lds_tile, s>>>(tm, pg, regions, fill, f->bitmap, f->pristine ? 1 : 0);
-    } else {
-        HIP_TRY(allow_lds(k_tile_build<false>, lds_tile));
-        k_tile_build<false><<<B, 1024, lds_tile, s>>>(tm, pg, regions, fill, f->bitmap, f->pristine ? 1 : 0);
-    }
-    CHECK_LAUNCH();
-    f->last_build_detail = (pg.ring ? PBF_DETAIL_RING : PBF_DETAIL_SORT) | (pg.sb << 8) | ((pg.kps / 256) << 12);
+    HIP_TRY(allow_lds(k_tile_build, lds_tile));
+    k_tile_build<<<B, 1024, lds_tile, s>>>(tm, pg, regions, fill, f->bitmap, f->pristine ? 1 : 0);
+    LAUNCHED(f, "k_tile_build");
+    f->last_build_detail = (pg.ring ? PBF_DETAIL_RING : PBF_DETAIL_SORT) | ((pg.kps / 256) << 12);
     k_ovf_build<<<256, 256, 0, s>>>(tm, ovf, ovf_count, f->bitmap, ovf_next);
-    CHECK_LAUNCH();
+    LAUNCHED(f, "k_ovf_build");
     f->pristine = false;
     return PBF_OK;
 }
 
 // Tiled probe of one key batch against nf filters sharing (m, k) (nf = 1: a plain probe).  The
 // keys are hashed and partitioned once, on f's stream with f's scratch (f = the set's first
-// filter, also for every later group of a large set); the tile test and the gather then run
-// once per filter.  hitmasks[i] + hm_off is filter i's output.
-// sc_ / st_: another scratch set and stream than f's (the overlapped chunks of probe_device);
-// after_part: recorded on the stream right after the partition launch.
+// filter, also for every later group of a large set); the tile test runs once per filter and
+// (ring partition) ONE gather serves every filter.  hitmasks[i] + hm_off is filter i's output.
 int run_tiled_probe_set(pbf_filter_t* f, pbf_filter_t* const* fs, uint32_t nf, const Batch& b,
-                        uint8_t* const* hitmasks, uint64_t hm_off, Scratch* sc_ = nullptr,
-                        hipStream_t st_ = nullptr, hipEvent_t after_part = nullptr) {
-    Scratch* const sc = sc_ ? sc_ : f->sc;
+                        uint8_t* const* hitmasks, uint64_t hm_off) {
+    Scratch* const sc = f->sc;
     const TileMap& tm = f->tm;
     const uint32_t B = tm.nbuckets;
     const uint32_t k = f->k;
@@ -990,7 +835,7 @@ int run_tiled_probe_set(pbf_filter_t* f, pbf_filter_t* const* fs, uint32_t nf, c
     auto* subcnt = static_cast<uint32_t*>(sc->subcnt.p);
     auto* R = static_cast<uint32_t*>(sc->rbits.p);
     auto* neg = static_cast<uint32_t*>(sc->neg.p);
-    hipStream_t s = st_ ? st_ : f->stream;
+    hipStream_t s = f->stream;
     // gather split over S tile ranges (several small workgroups per CU)
     const uint32_t S = pl.gsplit;
     const bool use_hw = S > 1 || nfg > 1;
@@ -1014,90 +859,73 @@ int run_tiled_probe_set(pbf_filter_t* f, pbf_filter_t* const* fs, uint32_t nf, c
     auto tprobe = expand ? k_tile_probe<true> : k_tile_probe<false>;
     auto tprobe_set = expand ? k_tile_probe_set<true> : k_tile_probe_set<false>;
     HIP_TRY(allow_lds(tprobe, lds_tile));
-    // One probe round: seeds [sbase, sbase + kr) of the keys `alive` marks (all if null), each
-    // filter's round hit mask (AND alive) into outs[i] + hm_off.
-    auto round = [&](int sbase, uint32_t kr, const uint32_t* alive, uint8_t* const* outs) -> int {
-        // the ring partition zeroes neg (and presets hw for the first filter) itself
-        if (!pg.ring) HIP_TRY(hipMemsetAsync(neg, 0, neg_bytes * nf, s));
-        hipError_t err = hipSuccess;
-        dispatch(kmax_for(kr), b.km, [&](auto KMAX, auto KM) {
-            if constexpr (decltype(KMAX)::value > 0) {
-                constexpr int KX = decltype(KMAX)::value, KMD = decltype(KM)::value;
-                if (pg.ring) {
-                    if constexpr (KX <= 16) {
-                        with_ring_kernel<KX, KMD, true>(kr, pg.ring, pg.cap, ring_pow2(tm), [&](auto kern) {
-                            err = allow_lds(kern, pl.lds_part);
-                            if (err == hipSuccess)
-                                kern<<<pg.G, kPartThreads, pl.lds_part, s>>>(b.ks, b.n, int(kr), tm, pg, regions,
-                                                                     fill, subcnt, nullptr, nullptr, ps, sbase,
-                                                                     alive, use_hw ? hw : nullptr);
-                        });
-                    }
-                } else {
-                    with_part_kernel<KX, KMD, true>(kr, [&](auto kern) {
+    // the ring partition zeroes neg (and presets hw for the fused gather) itself
+    if (!pg.ring) HIP_TRY(hipMemsetAsync(neg, 0, neg_bytes * nf, s));
+    hipError_t err = hipSuccess;
+    dispatch(kmax_for(k), b.km, [&](auto KMAX, auto KM) {
+        if constexpr (decltype(KMAX)::value > 0) {
+            constexpr int KX = decltype(KMAX)::value, KMD = decltype(KM)::value;
+            if (pg.ring) {
+                if constexpr (KX <= 16) {
+                    with_ring_kernel<KX, KMD, true>(k, ring_pow2(tm), [&](auto kern) {
                         err = allow_lds(kern, pl.lds_part);
                         if (err == hipSuccess)
-                            kern<<<pg.G, kPartThreads, pl.lds_part, s>>>(b.ks, b.n, int(kr), tm, pg, regions, fill,
-                                                                 subcnt, nullptr, nullptr, ps);
+                            kern<<<pg.G, kPartThreads, pl.lds_part, s>>>(b.ks, b.n, int(k), tm, pg, regions, fill, subcnt,
+                                                                 nullptr, nullptr, ps, use_hw ? hw : nullptr);
                     });
                 }
-            }
-        });
-        HIP_TRY(err);
-        CHECK_LAUNCH();
-        if (after_part) HIP_TRY(hipEventRecord(after_part, s));
-        auto gring = nf > 1 ? k_gather_ring<kMaxProbeSet> : k_gather_ring<1>;
-        if (pg.ring) HIP_TRY(allow_lds(gring, pl.lds_gather));
-        else HIP_TRY(allow_lds(k_gather, pl.lds_gather));
-        const dim3 grid(pg.G, S);
-        if (pg.ring) {
-            // every filter's tile test (one XCD-aware launch for a set), then ONE gather over
-            // the shared region entries
-            if (nf == 1) {
-                tprobe<<<B, 1024, lds_tile, s>>>(tm, pg, regions, fill, fs[0]->bitmap, R);
             } else {
-                HIP_TRY(allow_lds(tprobe_set, lds_tile));
-                const uint32_t grid = ((B + 7) / 8) * 8 * nf;
-                tprobe_set<<<grid, 1024, lds_tile, s>>>(tm, pg, regions, fill, ps, R, r_words);
+                with_part_kernel<KX, KMD, true>(k, [&](auto kern) {
+                    err = allow_lds(kern, pl.lds_part);
+                    if (err == hipSuccess)
+                        kern<<<pg.G, kPartThreads, pl.lds_part, s>>>(b.ks, b.n, int(k), tm, pg, regions, fill, subcnt,
+                                                             nullptr, nullptr, ps);
+                });
             }
-            CHECK_LAUNCH();
-            gring<<<grid, 512, pl.lds_gather, s>>>(tm, pg, b.n, regions, R, fill, subcnt, neg, alive, outs[0] + hm_off,
-                                                  hw, nf, r_words, neg_words, pl.gtq, gather_packed());
-            CHECK_LAUNCH();
-            if (use_hw) {
-                for (uint32_t i = 0; i < nf; ++i) {
-                    k_hw_to_hitmask<<<grid_for(neg_words, 256, 4096), 256, 0, s>>>(hw + i * neg_words, b.n,
-                                                                                   outs[i] + hm_off);
-                    CHECK_LAUNCH();
-                }
-            }
-            return PBF_OK;
         }
-        for (uint32_t i = 0; i < nf; ++i) {
-            if (S > 1) HIP_TRY(hipMemsetAsync(hw, 0xFF, neg_bytes, s));
-            tprobe<<<B, 1024, lds_tile, s>>>(tm, pg, regions, fill, fs[i]->bitmap, R);
-            CHECK_LAUNCH();
-            k_gather<<<grid, 512, pl.lds_gather, s>>>(tm, pg, b.n, regions, R, subcnt, neg + i * neg_words,
-                                                      outs[i] + hm_off, hw);
-            CHECK_LAUNCH();
-            if (S > 1) {
-                k_hw_to_hitmask<<<grid_for(neg_words, 256, 4096), 256, 0, s>>>(hw, b.n, outs[i] + hm_off);
-                CHECK_LAUNCH();
+    });
+    HIP_TRY(err);
+    LAUNCHED(f, pg.ring ? "k_part_ring<probe>" : "k_part<probe>");
+    const dim3 grid(pg.G, S);
+    if (pg.ring) {
+        auto gring = nf > 1 ? k_gather_ring<kMaxProbeSet> : k_gather_ring<1>;
+        HIP_TRY(allow_lds(gring, pl.lds_gather));
+        // every filter's tile test (one XCD-aware launch for a set), then ONE gather over the
+        // shared region entries
+        if (nf == 1) {
+            tprobe<<<B, 1024, lds_tile, s>>>(tm, pg, regions, fill, fs[0]->bitmap, R);
+        } else {
+            HIP_TRY(allow_lds(tprobe_set, lds_tile));
+            const uint32_t tgrid = ((B + 7) / 8) * 8 * nf;
+            tprobe_set<<<tgrid, 1024, lds_tile, s>>>(tm, pg, regions, fill, ps, R, r_words);
+        }
+        LAUNCHED(f, nf == 1 ? "k_tile_probe" : "k_tile_probe_set");
+        gring<<<grid, 512, pl.lds_gather, s>>>(tm, pg, b.n, regions, R, fill, subcnt, neg, hitmasks[0] + hm_off, hw, nf,
+                                              r_words, neg_words, pl.gtq);
+        LAUNCHED(f, "k_gather_ring");
+        if (use_hw) {
+            for (uint32_t i = 0; i < nf; ++i) {
+                k_hw_to_hitmask<<<grid_for(neg_words, 256, 4096), 256, 0, s>>>(hw + i * neg_words, b.n,
+                                                                               hitmasks[i] + hm_off);
+                LAUNCHED(f, "k_hw_to_hitmask");
             }
         }
         return PBF_OK;
-    };
-    if (nf > 1 || !pg.ring || k < 2 || probe_rounds() < 2) return round(0, k, nullptr, hitmasks);
-    // two rounds: seed 0 for every key, then seeds 1..k-1 for the keys seed 0 left alive
-    HIP_TRY(sc->alive.ensure(neg_bytes));
-    auto* alive = static_cast<uint32_t*>(sc->alive.p);
-    uint8_t* alive_out[1] = {reinterpret_cast<uint8_t*>(alive)};
-    const uint64_t keep_off = hm_off;
-    hm_off = 0;
-    int rc = round(0, 1, nullptr, alive_out);
-    if (rc) return rc;
-    hm_off = keep_off;
-    return round(1, k - 1, alive, hitmasks);
+    }
+    HIP_TRY(allow_lds(k_gather, pl.lds_gather));
+    for (uint32_t i = 0; i < nf; ++i) {
+        if (S > 1) HIP_TRY(hipMemsetAsync(hw, 0xFF, neg_bytes, s));
+        tprobe<<<B, 1024, lds_tile, s>>>(tm, pg, regions, fill, fs[i]->bitmap, R);
+        LAUNCHED(f, "k_tile_probe");
+        k_gather<<<grid, 512, pl.lds_gather, s>>>(tm, pg, b.n, regions, R, subcnt, neg + i * neg_words,
+                                                  hitmasks[i] + hm_off, hw);
+        LAUNCHED(f, "k_gather");
+        if (S > 1) {
+            k_hw_to_hitmask<<<grid_for(neg_words, 256, 4096), 256, 0, s>>>(hw, b.n, hitmasks[i] + hm_off);
+            LAUNCHED(f, "k_hw_to_hitmask");
+        }
+    }
+    return PBF_OK;
 }
 
 int run_tiled_probe(pbf_filter_t* f, const Batch& b, uint8_t* hitmask) {
@@ -1133,12 +961,11 @@ bool want_tiled_probe(pbf_filter_t* f, uint64_t n) {
     return f->words * 4 > (uint64_t(8) << 20) && npos >= (uint64_t(1) << 20) && npos * 16 >= f->words * 4;
 }
 
-// Largest probe batch one tiled pipeline takes: k_gather keeps a u16 run-boundary table
+// Largest probe batch one tiled pipeline takes: the gather keeps a u16 run-boundary table
 // (B x (nsub+1)) and a bit per key of its workgroup in LDS, and positions stay u32.
 uint64_t tiled_probe_batch(pbf_filter_t* f, int km, uint32_t nf = 1) {
     const uint32_t k = f->k;
     uint64_t n = std::max<uint64_t>(64, (kMaxPositions / k) & ~uint64_t(63));
-    if (probe_chunk()) n = std::min(n, probe_chunk());
     for (;;) {
         const PartPlan pl = plan_for(f->tm, k, km, n, true, nf);
         if ((pl.lds_gather <= 156 * 1024 && pl.pg.cap <= 65535) || n <= 64 * 1024) return n;
@@ -1152,13 +979,7 @@ int add_device(pbf_filter_t* f, const Batch& b) {
         // positions are indexed by u32 inside one pipeline: batch very large inputs
         const uint64_t per = std::max<uint64_t>(1, kMaxPositions / f->k);
         for (uint64_t i0 = 0; i0 < b.n; i0 += per) {
-            Batch c = b;
-            c.n = std::min<uint64_t>(per, b.n - i0);
-            if (b.km == kVar)
-                c.ks.offsets = b.ks.offsets + i0;  // off0 unchanged: offsets stay relative to it
-            else
-                c.ks.data = b.ks.data + i0 * b.ks.key_len;
-            int rc = run_tiled(f, c);
+            int rc = run_tiled(f, slice(b, i0, std::min<uint64_t>(per, b.n - i0)));
             if (rc) return rc;
         }
         f->last_mode = PBF_BUILD_TILED;
@@ -1168,63 +989,14 @@ int add_device(pbf_filter_t* f, const Batch& b) {
     return run_atomic(f, b);
 }
 
-// C chunks of a tiled probe (see probe_overlap): chunk c runs on stream c % 2 (f's stream or the
-// device's side stream) with that stream's scratch set; its partition waits for chunk c-1's.
-int probe_overlapped(pbf_filter_t* f, const Batch& b, uint8_t* hitmask_dev, uint32_t C) {
-    hipStream_t side = nullptr;
-    HIP_TRY(side_stream(f->device, &side));
-    if (!f->ev_part) HIP_TRY(hipEventCreateWithFlags(&f->ev_part, hipEventDisableTiming));
-    if (!f->ev_side) HIP_TRY(hipEventCreateWithFlags(&f->ev_side, hipEventDisableTiming));
-    // the side stream starts after everything already queued on f's stream (keys, builds)
-    HIP_TRY(hipEventRecord(f->ev_side, f->stream));
-    HIP_TRY(hipStreamWaitEvent(side, f->ev_side, 0));
-    Scratch* sc2 = nullptr;
-    int rc = lease_set(f->device, side, &sc2);
-    if (rc) return rc;
-    const uint64_t per = (((b.n + C - 1) / C) + 63) & ~uint64_t(63);
-    pbf_filter_t* fs[1] = {f};
-    uint32_t c = 0;
-    for (uint64_t i0 = 0; i0 < b.n && rc == PBF_OK; i0 += per, ++c) {
-        Batch cb = b;
-        cb.n = std::min<uint64_t>(per, b.n - i0);
-        if (b.km == kVar)
-            cb.ks.offsets = b.ks.offsets + i0;
-        else
-            cb.ks.data = b.ks.data + i0 * b.ks.key_len;
-        const bool on_side = c & 1;
-        hipStream_t st = on_side ? side : f->stream;
-        if (c > 0) {  // after the previous chunk's partition
-            const hipError_t e = hipStreamWaitEvent(st, f->ev_part, 0);
-            if (e != hipSuccess) { rc = fail(PBF_ERR_HIP, hipGetErrorString(e)); break; }
-        }
-        uint8_t* outs[1] = {hitmask_dev + i0 / 8};
-        rc = run_tiled_probe_set(f, fs, 1, cb, outs, 0, on_side ? sc2 : f->sc, st, f->ev_part);
-    }
-    // f's stream joins the side stream; the side set's next user orders after this call
-    return_set(f->device, sc2, side);
-    if (rc) return rc;
-    HIP_TRY(hipEventRecord(f->ev_side, side));
-    HIP_TRY(hipStreamWaitEvent(f->stream, f->ev_side, 0));
-    f->last_probe_mode = PBF_PROBE_TILED;
-    return PBF_OK;
-}
-
 int probe_device(pbf_filter_t* f, const Batch& b, uint8_t* hitmask_dev) {
     if (b.n == 0) return PBF_OK;
     int rc = materialise(f);
     if (rc) return rc;
     if (want_tiled_probe(f, b.n)) {
         const uint64_t per = tiled_probe_batch(f, b.km);
-        const uint32_t C = probe_overlap();
-        if (C >= 2 && b.n >= uint64_t(C) << 20 && b.n <= per) return probe_overlapped(f, b, hitmask_dev, C);
         for (uint64_t i0 = 0; i0 < b.n; i0 += per) {
-            Batch c = b;
-            c.n = std::min<uint64_t>(per, b.n - i0);
-            if (b.km == kVar)
-                c.ks.offsets = b.ks.offsets + i0;
-            else
-                c.ks.data = b.ks.data + i0 * b.ks.key_len;
-            rc = run_tiled_probe(f, c, hitmask_dev + i0 / 8);
+            rc = run_tiled_probe(f, slice(b, i0, std::min<uint64_t>(per, b.n - i0)), hitmask_dev + i0 / 8);
             if (rc) return rc;
         }
         f->last_probe_mode = PBF_PROBE_TILED;
@@ -1233,9 +1005,9 @@ int probe_device(pbf_filter_t* f, const Batch& b, uint8_t* hitmask_dev) {
     const uint32_t grid = grid_for(b.n, 256, 1u << 20);
     dispatch(kmax_for(f->k), b.km, [&](auto KMAX, auto KM) {
         k_probe<decltype(KMAX)::value, decltype(KM)::value>
-            <<<grid, 256, 0, f->stream>>>(b.ks, b.n, int(f->k), f->im, f->bitmap, hitmask_dev, probe_stage1());
+            <<<grid, 256, 0, f->stream>>>(b.ks, b.n, int(f->k), f->im, f->bitmap, hitmask_dev, kProbeStage1);
     });
-    CHECK_LAUNCH();
+    LAUNCHED(f, "k_probe");
     f->last_probe_mode = PBF_PROBE_DIRECT;
     f->last_probe_detail = 0;
     return PBF_OK;
@@ -1257,37 +1029,65 @@ bool shared_probe(pbf_filter_t* const* fs, uint32_t nf, uint64_t n) {
     return want_tiled_probe(fs[0], n);
 }
 
+// Filters of a set that take the fused direct probe (k_probe_set): those whose own probe would be
+// the direct one for this batch (small filters: an LSM's SSTables of a few MB), grouped by k.
+bool set_direct(pbf_filter_t* f, uint64_t n) {
+    return kmax_for(f->k) > 0 && (f->probe_mode == PBF_PROBE_DIRECT || !want_tiled_probe(f, n));
+}
+
+// One launch of k_probe_set per (k, up to 64 filters): every key is hashed once for the group.
+int probe_set_direct(pbf_filter_t* f0, std::vector<pbf_filter_t*>& grp, std::vector<uint8_t*>& hms, const Batch& b) {
+    const uint32_t k = grp[0]->k;
+    for (size_t g0 = 0; g0 < grp.size(); g0 += kMaxFilterSet) {
+        FilterSet fset{};
+        fset.nf = uint32_t(std::min<size_t>(kMaxFilterSet, grp.size() - g0));
+        for (uint32_t i = 0; i < fset.nf; ++i) {
+            fset.bm[i] = grp[g0 + i]->bitmap;
+            fset.im[i] = grp[g0 + i]->im;
+            fset.hm[i] = hms[g0 + i];
+        }
+        const uint32_t grid = grid_for(b.n, 256, 1u << 20);
+        dispatch(kmax_for(k), b.km, [&](auto KMAX, auto KM) {
+            if constexpr (decltype(KMAX)::value > 0)
+                k_probe_set<decltype(KMAX)::value, decltype(KM)::value>
+                    <<<grid, 256, 0, f0->stream>>>(b.ks, b.n, int(k), fset);
+        });
+        LAUNCHED(f0, "k_probe_set");
+    }
+    for (pbf_filter_t* f : grp) {
+        f->last_probe_mode = PBF_PROBE_DIRECT;
+        f->last_probe_detail = PBF_DETAIL_SET | (uint32_t(std::min<size_t>(grp.size(), kMaxFilterSet)) << 8);
+    }
+    return PBF_OK;
+}
+
 // Device keys / hit masks; asynchronous on fs[0]'s stream.  Every other filter's stream first
 // hands its pending work (a build, a from_bytes) to fs[0]'s stream and afterwards waits for the
 // probe, so later calls on any handle are ordered after it.
+//   * every filter of one (nb_bytes, k), tiled: ONE partition for the set (run_tiled_probe_set);
+//   * otherwise the filters whose own probe would be direct go through k_probe_set, grouped by
+//     k (mixed sizes: each key hashed once for the group), and the rest (large filters of
+//     distinct sizes) each through its own pipeline on fs[0]'s stream.
 int probe_multi_device(pbf_filter_t* const* fs, uint32_t nf, const Batch& b, uint8_t* const* hitmasks) {
     pbf_filter_t* f0 = fs[0];
     hipStream_t s0 = f0->stream;
     int rc = materialise(f0);
     if (rc) return rc;
     HIP_TRY(filter_event(f0));
-    const bool shared = shared_probe(fs, nf, b.n);
-    if (!shared) HIP_TRY(hipEventRecord(f0->ev, s0));  // keys ready on s0
     for (uint32_t i = 1; i < nf; ++i) {
         pbf_filter_t* fi = fs[i];
         rc = materialise(fi);
         if (rc) return rc;
         HIP_TRY(filter_event(fi));
-        if (!shared) HIP_TRY(hipStreamWaitEvent(fi->stream, f0->ev, 0));
-    }
-    if (shared) {
-        for (uint32_t i = 1; i < nf; ++i) {
-            HIP_TRY(hipEventRecord(fs[i]->ev, fs[i]->stream));
-            HIP_TRY(hipStreamWaitEvent(s0, fs[i]->ev, 0));
+        if (fi->stream != s0) {
+            HIP_TRY(hipEventRecord(fi->ev, fi->stream));
+            HIP_TRY(hipStreamWaitEvent(s0, fi->ev, 0));
         }
+    }
+    if (shared_probe(fs, nf, b.n)) {
         const uint64_t per = tiled_probe_batch(f0, b.km, std::min<uint32_t>(nf, kMaxProbeSet));
         for (uint64_t i0 = 0; i0 < b.n; i0 += per) {
-            Batch c = b;
-            c.n = std::min<uint64_t>(per, b.n - i0);
-            if (b.km == kVar)
-                c.ks.offsets = b.ks.offsets + i0;
-            else
-                c.ks.data = b.ks.data + i0 * b.ks.key_len;
+            const Batch c = slice(b, i0, std::min<uint64_t>(per, b.n - i0));
             for (uint32_t g0 = 0; g0 < nf; g0 += kMaxProbeSet) {
                 rc = run_tiled_probe_set(f0, fs + g0, std::min<uint32_t>(kMaxProbeSet, nf - g0), c, hitmasks + g0,
                                          i0 / 8);
@@ -1299,25 +1099,56 @@ int probe_multi_device(pbf_filter_t* const* fs, uint32_t nf, const Batch& b, uin
             fs[i]->last_probe_detail = f0->last_probe_detail;
         }
     } else {
-        // each filter on its own stream and scratch set (fs[0] uses the caller's lease),
-        // joined back into fs[0]'s
+        // direct groups by k (in first-appearance order), then the per-filter pipelines
+        std::vector<uint32_t> ks;
+        std::vector<uint32_t> rest;
         for (uint32_t i = 0; i < nf; ++i) {
-            if (i == 0) {
-                rc = probe_device(fs[0], b, hitmasks[0]);
-            } else {
-                Lease li(fs[i]);
-                rc = li.acquire();
-                if (!rc) rc = probe_device(fs[i], b, hitmasks[i]);
+            if (!set_direct(fs[i], b.n)) {
+                rest.push_back(i);
+            } else if (std::find(ks.begin(), ks.end(), fs[i]->k) == ks.end()) {
+                ks.push_back(fs[i]->k);
             }
+        }
+        for (uint32_t k : ks) {
+            std::vector<pbf_filter_t*> grp;
+            std::vector<uint8_t*> hms;
+            for (uint32_t i = 0; i < nf; ++i)
+                if (fs[i]->k == k && set_direct(fs[i], b.n)) {
+                    grp.push_back(fs[i]);
+                    hms.push_back(hitmasks[i]);
+                }
+            rc = probe_set_direct(f0, grp, hms, b);
             if (rc) return rc;
         }
-        for (uint32_t i = 1; i < nf; ++i) {
-            HIP_TRY(hipEventRecord(fs[i]->ev, fs[i]->stream));
-            HIP_TRY(hipStreamWaitEvent(s0, fs[i]->ev, 0));
+        if (!rest.empty()) {
+            // the large filters of distinct sizes: each its own pipeline on its own stream and
+            // scratch set (fs[0] with the caller's lease), after the keys are ready on s0, then
+            // joined back into s0
+            HIP_TRY(hipEventRecord(f0->ev, s0));
+            for (uint32_t i : rest)
+                if (fs[i]->stream != s0) HIP_TRY(hipStreamWaitEvent(fs[i]->stream, f0->ev, 0));
+            for (uint32_t i : rest) {
+                if (i == 0) {
+                    rc = probe_device(f0, b, hitmasks[0]);
+                } else {
+                    Lease li(fs[i]);
+                    rc = li.acquire();
+                    if (!rc) rc = probe_device(fs[i], b, hitmasks[i]);
+                }
+                if (rc) return rc;
+            }
+            for (uint32_t i : rest) {
+                if (fs[i]->stream == s0) continue;
+                HIP_TRY(hipEventRecord(fs[i]->ev, fs[i]->stream));
+                HIP_TRY(hipStreamWaitEvent(s0, fs[i]->ev, 0));
+            }
         }
     }
     HIP_TRY(hipEventRecord(f0->ev, s0));
-    for (uint32_t i = 1; i < nf; ++i) HIP_TRY(hipStreamWaitEvent(fs[i]->stream, f0->ev, 0));
+    for (uint32_t i = 1; i < nf; ++i) {
+        if (fs[i]->stream != s0) HIP_TRY(hipStreamWaitEvent(fs[i]->stream, f0->ev, 0));
+        fs[i]->pending = true;
+    }
     return PBF_OK;
 }
 
@@ -1328,7 +1159,7 @@ int hash_device(pbf_filter_t* f, const Batch& b, uint64_t* out_dev) {
         k_hash_indices<decltype(KMAX)::value, decltype(KM)::value>
             <<<grid, 256, 0, f->stream>>>(b.ks, b.n, int(f->k), f->im, out_dev);
     });
-    CHECK_LAUNCH();
+    LAUNCHED(f, "k_hash_indices");
     return PBF_OK;
 }
 
@@ -1432,19 +1263,46 @@ int check_keys(pbf_filter_t* f, const uint8_t* keys, const uint64_t* offsets, ui
 // the results), then keeps polling with sleeps that back off from 10 us to 200 us, so a long
 // wait costs a host core almost nothing and does not depend on an interrupt-driven wake-up
 // (PBF_SPIN_US sets the pure polling budget, default 200 us).
+//
+// A wait has a deadline (PBF_WAIT_S seconds, default 60 — no call of this library runs for
+// more than a fraction of a second of GPU time; the GPU box's own silence limit is 3 minutes):
+// past it the call fails with PBF_ERR_HIP naming the stream and the last kernel enqueued on it,
+// instead of spinning silently.  (Round 2 saw one GPU-suite run hang inside a wait that blocked
+// on an event created with hipEventBlockingSync, i.e. on an interrupt-driven wake-up; no log of
+// the run was kept.  Every kernel's loops are bounded and its barriers uniform, and since the
+// blocking wait was replaced by polling no run has hung — but that is not proof, so the wait now
+// reports a stream that does not finish: DESIGN.md §1.)
 int wait_stream(pbf_filter_t* f) {
     static const long spin_us = [] {
         const char* e = std::getenv("PBF_SPIN_US");
         return e ? std::atol(e) : 200L;
     }();
+    static const double limit_s = [] {
+        const char* e = std::getenv("PBF_WAIT_S");
+        const double x = e ? std::atof(e) : 0.0;
+        return x > 0 ? x : 60.0;
+    }();
     const auto t0 = std::chrono::steady_clock::now();
+    const auto spin = std::chrono::microseconds(spin_us);
+    const auto limit = std::chrono::duration<double>(limit_s);
     long nap_us = 10;
     for (;;) {
         const hipError_t e = hipStreamQuery(f->stream);
-        if (e == hipSuccess) return PBF_OK;
+        if (e == hipSuccess) {
+            f->pending = false;
+            return PBF_OK;
+        }
         (void)hipGetLastError();  // "not ready" is not an error (see event_done)
         if (e != hipErrorNotReady) return fail(PBF_ERR_HIP, std::string("hipStreamQuery: ") + hipGetErrorString(e));
-        if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(spin_us)) {
+        const auto waited = std::chrono::steady_clock::now() - t0;
+        if (waited > limit) {
+            char msg[256];
+            std::snprintf(msg, sizeof msg,
+                          "stream %p of device %d did not finish within %.1f s (PBF_WAIT_S); last kernel enqueued: %s",
+                          static_cast<void*>(f->stream), f->device, limit_s, f->last_kernel);
+            return fail(PBF_ERR_HIP, msg);
+        }
+        if (waited > spin) {
             std::this_thread::sleep_for(std::chrono::microseconds(nap_us));
             nap_us = std::min(nap_us * 2, 200L);
         }
@@ -1599,6 +1457,12 @@ constexpr size_t kOneKeyOffs = 64, kOneKeyData = 128, kOneKeyMax = 4096;
 struct OneKeyStage {
     uint8_t* host = nullptr;
     uint8_t* dev = nullptr;
+    OneKeyStage() = default;
+    OneKeyStage(const OneKeyStage&) = delete;
+    OneKeyStage& operator=(const OneKeyStage&) = delete;
+    ~OneKeyStage() {  // the thread ends: its pinned stage goes back (reader pools churn threads)
+        if (host) (void)hipHostFree(host);
+    }
 };
 
 int one_key_stage(int device, OneKeyStage** out) {
@@ -1617,6 +1481,170 @@ int one_key_stage(int device, OneKeyStage** out) {
         st.dev = static_cast<uint8_t*>(d);
     }
     *out = &st;
+    return PBF_OK;
+}
+
+// BloomFilter.may_contain (bloom_filter.py:67-74) for one key; the caller holds f's lock.
+int may_contain_locked(pbf_filter_t* f, const uint8_t* key, uint64_t len, int* out) {
+    int rc = enter(f);
+    if (rc) return rc;
+    if (!out || (len && !key)) return fail(PBF_ERR_INVALID, "null key or out");
+    if (f->k == 0) {  // the AND over no bits (bloom_filter.py:71-74 runs no iteration)
+        *out = 1;
+        return PBF_OK;
+    }
+    rc = materialise(f);
+    if (rc) return rc;
+    if (len > kOneKeyMax) {  // long keys: the staged batch path
+        uint64_t offs[2] = {0, len};
+        uint8_t hm = 0;
+        LEASE(f);
+        rc = for_host_chunks(f, key, offs, 0, 1, 64, [&](const Batch& b, uint64_t) {
+            HIP_TRY(f->sc->dout.ensure(8));
+            int r = probe_device(f, b, static_cast<uint8_t*>(f->sc->dout.p));
+            if (r) return r;
+            HIP_TRY(hipMemcpyAsync(&hm, f->sc->dout.p, 1, hipMemcpyDeviceToHost, f->stream));
+            return PBF_OK;
+        });
+        if (rc) return rc;
+        WAIT(f);
+        *out = hm & 1;
+        return PBF_OK;
+    }
+    OneKeyStage* st = nullptr;
+    rc = one_key_stage(f->device, &st);
+    if (rc) return rc;
+    // the key and its two offsets go into mapped pinned memory the kernel reads over the bus;
+    // the kernel's hit byte comes back the same way: one launch, no copies
+    uint64_t* offs = reinterpret_cast<uint64_t*>(st->host + kOneKeyOffs);
+    offs[0] = 0;
+    offs[1] = len;
+    if (len) std::memcpy(st->host + kOneKeyData, key, len);
+    st->host[0] = 0xEE;
+    KeySet ks{};
+    ks.data = st->dev + kOneKeyData;
+    ks.offsets = reinterpret_cast<const uint64_t*>(st->dev + kOneKeyOffs);
+    ks.off0 = ks.offsets;
+    dispatch(kmax_for(f->k), kVar, [&](auto KMAX, auto KM) {
+        k_probe<decltype(KMAX)::value, decltype(KM)::value>
+            <<<1, 64, 0, f->stream>>>(ks, 1, int(f->k), f->im, f->bitmap, st->dev, int(f->k));
+    });
+    LAUNCHED(f, "k_probe<one key>");
+    // The kernel's hit byte lands in mapped host memory as soon as it is stored (the key bytes
+    // were read before it), which is earlier than the stream's completion signal: poll the byte,
+    // and fall back to the stream wait (which also reports a failed kernel) after 2 ms.
+    volatile uint8_t* res = reinterpret_cast<volatile uint8_t*>(st->host);
+    const auto t0 = std::chrono::steady_clock::now();
+    uint8_t hit = 0xEE;
+    for (uint32_t spin = 0;; ++spin) {
+        hit = *res;
+        if (hit != 0xEE) break;
+        if ((spin & 255) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) {
+            WAIT(f);
+            hit = *res;
+            break;
+        }
+    }
+    if (hit > 1) return fail(PBF_ERR_HIP, "one-key probe: result byte not written");
+    *out = hit;
+    f->last_probe_mode = PBF_PROBE_DIRECT;
+    f->last_probe_detail = PBF_DETAIL_ONE_KEY;
+    return PBF_OK;
+}
+
+// The filters' pending work (builds, from_bytes) ordered before work on stream s: a filter
+// whose stream may still run queued work and has not finished it hands it over by an event.
+int join_into(pbf_filter_t* f, hipStream_t s) {
+    if (!f->pending || f->stream == s) return PBF_OK;
+    const hipError_t q = hipStreamQuery(f->stream);
+    if (q == hipSuccess) {
+        f->pending = false;
+        return PBF_OK;
+    }
+    (void)hipGetLastError();  // "not ready"
+    HIP_TRY(filter_event(f));
+    HIP_TRY(hipEventRecord(f->ev, f->stream));
+    HIP_TRY(hipStreamWaitEvent(s, f->ev, 0));
+    return PBF_OK;
+}
+
+// LsmStorage.get's bloom checks for ONE key over a set of SSTable filters (src/lsm_storage.py:
+// 164-179: every L0 table, and each level table whose key range holds the key): one
+// k_may_contain_set launch per k and 64 filters, the key in and the answer out through mapped
+// pinned memory.  Bit i of out_bits (LSB-first) = filters[i]->may_contain(key).  The caller
+// holds every filter's lock.
+int may_contain_set_locked(pbf_filter_t* const* fs, uint32_t nf, const uint8_t* key, uint64_t len, uint8_t* out_bits) {
+    pbf_filter_t* f0 = fs[0];
+    int rc = enter(f0);
+    if (rc) return rc;
+    std::memset(out_bits, 0, (nf + 7) / 8);
+    auto put = [&](uint32_t i, bool hit) {
+        if (hit) out_bits[i >> 3] |= uint8_t(1u << (i & 7));
+    };
+    // filters the fused kernel does not take (k > 32, keys longer than the mapped stage): one
+    // may_contain each
+    std::vector<uint32_t> ks;
+    for (uint32_t i = 0; i < nf; ++i) {
+        pbf_filter_t* f = fs[i];
+        if (f->k == 0) {
+            put(i, true);  // the AND over no bits
+        } else if (kmax_for(f->k) == 0 || len > kOneKeyMax) {
+            int hit = 0;
+            rc = may_contain_locked(f, key, len, &hit);
+            if (rc) return rc;
+            put(i, hit != 0);
+        } else if (std::find(ks.begin(), ks.end(), f->k) == ks.end()) {
+            ks.push_back(f->k);
+        }
+    }
+    if (ks.empty()) return PBF_OK;
+    OneKeyStage* st = nullptr;
+    rc = one_key_stage(f0->device, &st);
+    if (rc) return rc;
+    if (len) std::memcpy(st->host + kOneKeyData, key, len);
+    hipStream_t s = f0->stream;
+    for (uint32_t k : ks) {
+        std::vector<uint32_t> idx;
+        for (uint32_t i = 0; i < nf; ++i)
+            if (fs[i]->k == k) idx.push_back(i);
+        for (size_t c0 = 0; c0 < idx.size(); c0 += kMaxFilterSet) {
+            FilterSet fset{};
+            fset.nf = uint32_t(std::min<size_t>(kMaxFilterSet, idx.size() - c0));
+            for (uint32_t j = 0; j < fset.nf; ++j) {
+                pbf_filter_t* f = fs[idx[c0 + j]];
+                rc = materialise(f);
+                if (rc) return rc;
+                rc = join_into(f, s);
+                if (rc) return rc;
+                fset.bm[j] = f->bitmap;
+                fset.im[j] = f->im;
+            }
+            volatile uint8_t* flag = st->host + 8;
+            *flag = 0;
+            dispatch(kmax_for(k), kVar, [&](auto KMAX, auto) {
+                if constexpr (decltype(KMAX)::value > 0)
+                    k_may_contain_set<decltype(KMAX)::value>
+                        <<<1, 64, 0, s>>>(st->dev + kOneKeyData, uint32_t(len), int(k), fset, st->dev);
+            });
+            LAUNCHED(f0, "k_may_contain_set");
+            // poll the flag the kernel sets after its answer (earlier than the stream's
+            // completion signal); the stream wait (which also reports a failed kernel) after 2 ms
+            const auto t0 = std::chrono::steady_clock::now();
+            for (uint32_t spin = 0; !*flag; ++spin) {
+                if ((spin & 255) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) {
+                    WAIT(f0);
+                    if (!*flag) return fail(PBF_ERR_HIP, "one-key set probe: answer not written");
+                    break;
+                }
+            }
+            const uint64_t bits = *reinterpret_cast<volatile uint64_t*>(st->host);
+            for (uint32_t j = 0; j < fset.nf; ++j) put(idx[c0 + j], (bits >> j) & 1u);
+        }
+    }
+    for (uint32_t i = 0; i < nf; ++i) {
+        fs[i]->last_probe_mode = PBF_PROBE_DIRECT;
+        fs[i]->last_probe_detail = PBF_DETAIL_ONE_KEY | PBF_DETAIL_SET;
+    }
     return PBF_OK;
 }
 
@@ -1697,19 +1725,15 @@ int pbf_create(int device, uint64_t nb_bytes, uint32_t nb_hash_functions, pbf_fi
 int pbf_destroy(pbf_filter_t* f) {
     if (!f) return PBF_OK;
     (void)hipSetDevice(f->device);
+    // Everything that reads this filter's bitmap is ordered before the end of its stream: its
+    // own calls run there, and a multi-filter probe that read it on another filter's stream made
+    // this stream wait for that probe (probe_multi_device's closing joins).  So after this sync
+    // the bitmap can go back to the recycle cache.  (Scratch sets keep their last_stream: pooled
+    // streams are never destroyed, so a later lease from another stream still waits on the
+    // set's event.)
     if (f->stream) (void)hipStreamSynchronize(f->stream);
-    {
-        // scratch sets last used on this stream: their work is done (synchronised above), and
-        // the stream handle may be reused by a later filter
-        DevicePool& pool = device_pool(f->device);
-        std::lock_guard<std::mutex> lock(pool.mu);
-        for (Scratch* sc : pool.sets)
-            if (sc->last_stream == f->stream) sc->last_stream = nullptr;
-    }
     if (f->bitmap) bitmap_release(f->device, bitmap_alloc_bytes(f->alloc_words), f->bitmap);
     if (f->ev) (void)hipEventDestroy(f->ev);
-    if (f->ev_part) (void)hipEventDestroy(f->ev_part);
-    if (f->ev_side) (void)hipEventDestroy(f->ev_side);
     delete f;  // the stream belongs to the device's pool
     return PBF_OK;
 }
@@ -1717,6 +1741,13 @@ int pbf_destroy(pbf_filter_t* f) {
 int pbf_trim(int device) {
     HIP_TRY(hipSetDevice(device));
     bitmap_cache_trim(device);
+    {
+        // the cached bitmaps went back to the device's stream-ordered pool (release threshold
+        // raised, bitmap_alloc): hand its free blocks back to the device
+        hipMemPool_t pool = nullptr;
+        if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess) HIP_TRY(hipMemPoolTrimTo(pool, 0));
+        else (void)hipGetLastError();
+    }
     DevicePool& pool = device_pool(device);
     std::lock_guard<std::mutex> lock(pool.mu);
     for (Scratch* sc : pool.sets) {
@@ -1733,8 +1764,7 @@ int pbf_scratch_bytes(int device, uint64_t* out) {
     std::lock_guard<std::mutex> lock(pool.mu);
     uint64_t t = 0;
     for (Scratch* sc : pool.sets)
-        for (const DevBuf* d : {&sc->regions, &sc->fill, &sc->ovf, &sc->ovf_count, &sc->subcnt, &sc->rbits, &sc->neg,
-                                &sc->alive, &sc->hw, &sc->dkeys, &sc->doffs, &sc->dout, &sc->svals, &sc->splan,
+        for (const DevBuf* d : {&sc->regions, &sc->fill, &sc->ovf, &sc->ovf_count, &sc->subcnt, &sc->rbits, &sc->neg, &sc->hw, &sc->dkeys, &sc->doffs, &sc->dout, &sc->svals, &sc->splan,
                                 &sc->ssec, &sc->serr})
             t += d->bytes;
     *out = t;
@@ -1745,6 +1775,7 @@ int pbf_clear(pbf_filter_t* f) {
     LOCK(f);
     int rc = enter(f);
     if (rc) return rc;
+    f->pending = true;
     if (f->tiled_ok) {
         // The next tiled build rewrites every reachable word; a read or an atomic build
         // materialises the zero bitmap first.  Only a from_bytes() can have dirtied the
@@ -1869,7 +1900,7 @@ int pbf_popcount(pbf_filter_t* f, uint64_t* out) {
     HIP_TRY(hipMemsetAsync(f->dpop, 0, 8, f->stream));
     k_popcount<<<grid_for(f->alloc_words, 256, 4096), 256, 0, f->stream>>>(
         f->bitmap, f->alloc_words, reinterpret_cast<unsigned long long*>(f->dpop));
-    CHECK_LAUNCH();
+    LAUNCHED(f, "k_popcount");
     HIP_TRY(hipMemcpyAsync(out, f->dpop, 8, hipMemcpyDeviceToHost, f->stream));
     WAIT(f);
     return PBF_OK;
@@ -1902,70 +1933,25 @@ int pbf_murmur3_x86_32(int device, const uint8_t* key, uint64_t len, uint32_t se
 
 int pbf_may_contain(pbf_filter_t* f, const uint8_t* key, uint64_t len, int* out) {
     LOCK(f);
-    int rc = enter(f);
-    if (rc) return rc;
-    if (!out || (len && !key)) return fail(PBF_ERR_INVALID, "null key or out");
-    if (f->k == 0) {  // the AND over no bits (bloom_filter.py:71-74 runs no iteration)
-        *out = 1;
-        return PBF_OK;
+    return may_contain_locked(f, key, len, out);
+}
+
+int pbf_may_contain_set(pbf_filter_t* const* filters, uint32_t nfilters, const uint8_t* key, uint64_t len,
+                        uint8_t* out_bits) {
+    if (nfilters == 0) return PBF_OK;
+    if (!filters || !out_bits || (len && !key)) return fail(PBF_ERR_INVALID, "null pointer");
+    for (uint32_t i = 0; i < nfilters; ++i) {
+        if (!filters[i]) return fail(PBF_ERR_INVALID, "null filter handle in set");
+        if (filters[i]->device != filters[0]->device) return fail(PBF_ERR_INVALID, "filters of one set must share a device");
     }
-    rc = materialise(f);
-    if (rc) return rc;
-    if (len > kOneKeyMax) {  // long keys: the staged batch path
-        uint64_t offs[2] = {0, len};
-        uint8_t hm = 0;
-        LEASE(f);
-        rc = for_host_chunks(f, key, offs, 0, 1, 64, [&](const Batch& b, uint64_t) {
-            HIP_TRY(f->sc->dout.ensure(8));
-            int r = probe_device(f, b, static_cast<uint8_t*>(f->sc->dout.p));
-            if (r) return r;
-            HIP_TRY(hipMemcpyAsync(&hm, f->sc->dout.p, 1, hipMemcpyDeviceToHost, f->stream));
-            return PBF_OK;
-        });
-        if (rc) return rc;
-        WAIT(f);
-        *out = hm & 1;
-        return PBF_OK;
-    }
-    OneKeyStage* st = nullptr;
-    rc = one_key_stage(f->device, &st);
-    if (rc) return rc;
-    // the key and its two offsets go into mapped pinned memory the kernel reads over the bus;
-    // the kernel's hit byte comes back the same way: one launch, no copies
-    uint64_t* offs = reinterpret_cast<uint64_t*>(st->host + kOneKeyOffs);
-    offs[0] = 0;
-    offs[1] = len;
-    if (len) std::memcpy(st->host + kOneKeyData, key, len);
-    st->host[0] = 0xEE;
-    KeySet ks{};
-    ks.data = st->dev + kOneKeyData;
-    ks.offsets = reinterpret_cast<const uint64_t*>(st->dev + kOneKeyOffs);
-    ks.off0 = ks.offsets;
-    dispatch(kmax_for(f->k), kVar, [&](auto KMAX, auto KM) {
-        k_probe<decltype(KMAX)::value, decltype(KM)::value>
-            <<<1, 64, 0, f->stream>>>(ks, 1, int(f->k), f->im, f->bitmap, st->dev, int(f->k));
-    });
-    CHECK_LAUNCH();
-    // The kernel's hit byte lands in mapped host memory as soon as it is stored (the key bytes
-    // were read before it), which is earlier than the stream's completion signal: poll the byte,
-    // and fall back to the stream wait (which also reports a failed kernel) after 2 ms.
-    volatile uint8_t* res = reinterpret_cast<volatile uint8_t*>(st->host);
-    const auto t0 = std::chrono::steady_clock::now();
-    uint8_t hit = 0xEE;
-    for (uint32_t spin = 0;; ++spin) {
-        hit = *res;
-        if (hit != 0xEE) break;
-        if ((spin & 255) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) {
-            WAIT(f);
-            hit = *res;
-            break;
-        }
-    }
-    if (hit > 1) return fail(PBF_ERR_HIP, "one-key probe: result byte not written");
-    *out = hit;
-    f->last_probe_mode = PBF_PROBE_DIRECT;
-    f->last_probe_detail = PBF_DETAIL_ONE_KEY;
-    return PBF_OK;
+    // every distinct handle of the set, in address order (a table may appear twice)
+    std::vector<pbf_filter_t*> order(filters, filters + nfilters);
+    std::sort(order.begin(), order.end());
+    order.erase(std::unique(order.begin(), order.end()), order.end());
+    std::vector<std::unique_lock<std::mutex>> locks;
+    locks.reserve(order.size());
+    for (pbf_filter_t* p : order) locks.emplace_back(p->mu);
+    return may_contain_set_locked(filters, nfilters, key, len, out_bits);
 }
 
 void* pbf_stream(pbf_filter_t* f) { return f ? static_cast<void*>(f->stream) : nullptr; }
@@ -2134,7 +2120,7 @@ int pbf_build_sstable(pbf_filter_t* f, const uint8_t* keys, const uint64_t* key_
     HIP_TRY(hipMemsetAsync(sc->serr.p, 0, 4, s));
     k_encode_blocks<<<uint32_t(nblocks), 512, kEncodeLds, s>>>(dk, dko, dv, dvo, dbf, dbo, static_cast<uint8_t*>(sc->ssec.p),
                                                                static_cast<unsigned int*>(sc->serr.p));
-    CHECK_LAUNCH();
+    LAUNCHED(f, "k_encode_blocks");
     if (f->k > 0) {  // SSTableBuilder.build's filter over every key (sstable.py:274)
         rc = add_device(f, make_batch(dk, dko, 0, n));
         if (rc) return rc;
@@ -2195,9 +2181,12 @@ int pbf_key_range_mask(int device, void* stream, const uint8_t* keys, const uint
     // table groups whose bounds fit the LDS stage (host-side sizes: the offsets are read on the
     // host for the host path, copied back first for the device path)
     std::vector<uint64_t> bo(2 * size_t(ntables) + 1);
-    if (on_device)
-        HIP_TRY(hipMemcpy(bo.data(), bound_offsets, bo.size() * 8, hipMemcpyDeviceToHost));
-    else
+    if (on_device) {
+        // ordered after whatever the caller queued on its stream (the offsets may come from it)
+        HIP_TRY(hipMemcpyAsync(bo.data(), bound_offsets, bo.size() * 8, hipMemcpyDeviceToHost,
+                               static_cast<hipStream_t>(stream)));
+        HIP_TRY(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+    } else
         std::memcpy(bo.data(), bound_offsets, bo.size() * 8);
     std::vector<std::pair<uint32_t, uint32_t>> groups;  // (t0, nt, words)
     std::vector<uint32_t> gwords;

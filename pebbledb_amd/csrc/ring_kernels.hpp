@@ -1,31 +1,29 @@
 // Ring-buffer partition for the LDS-tiled build / probe (reference semantics:
-// src/bloom_filter.py:60-74), gfx950.  Used when the bitmap has many tiles (B >= ~128k
-// positions per sub-chunk key... see plan_ring in pebblebloom.hip), e.g. C2: m = 2^30, B = 1024.
+// src/bloom_filter.py:60-74), gfx950.  Used when a bitmap has <= 1024 tiles and a 1024-key
+// sub-chunk puts only a few positions into each tile (plan_for in pebblebloom.hip), e.g. C2:
+// m = 2^30, B = 1024 tiles of 2^20 bits.
 //
 // Why: the counting-sort partition (k_part) appends each sub-chunk's per-tile run (~18 entries,
 // ~72 B at C2) to its region with lane-parallel dword stores.  A run starts and ends inside
 // 64-B segments, and the fabric sees every piece as its own write request (measured: 7.0M write
-// requests, half of them 32-B partials, for 240 MB of entries); the write-out phase then runs at
-// the fabric's request rate.  Here every tile keeps a small FIFO ring in LDS; a sub-chunk appends
-// its positions to the rings (one LDS atomic + one LDS store per position, no scan, no stage),
-// and a flush phase writes every complete GS-entry group (64 B at GS = 16) with ONE wave store
-// instruction (4 lanes x 16 B), so each region line leaves as whole 64-B requests.
+// requests, half of them 32-B partials, for 240 MB of entries).  Here every tile keeps a small
+// FIFO ring in LDS; a sub-chunk appends its positions to the rings (one LDS atomic + one LDS
+// store per position, no scan, no stage), and a flush phase writes every complete 16-entry group
+// with ONE wave store instruction (4 lanes x 16 B), so each region line leaves as whole 64-B
+// requests.
 //
-//   ring      RC entries per tile (RC = 2*GS).  head = entries flushed (= the region write
-//             cursor, a multiple of GS), tail = entries appended; packed in one u64 per tile.  Entry e of tile b sits at
-//             ring[b*RC + (e % RC)] and lands at region position e.
-//   sub-chunk 1024 keys (one per thread).  The host picks the geometry so a tile receives ~GS/3
-//             positions per sub-chunk; a position that would overrun the ring (or the region
-//             capacity) leaves the stream like k_part's overflow (build: overflow list; probe:
-//             tested against the bitmap in place, a miss clears the key via `neg`).
+//   ring      32 entries per tile (RC), groups of GS = 16.  head = entries flushed (= the region
+//             write cursor, a multiple of GS), tail = entries appended; packed as the 16-bit
+//             halves of one u32 per tile.  Entry e of tile b sits at ring[b*RC + (e % RC)] and
+//             lands at region position e.
+//   sub-chunk kps keys (<= 1024, one per thread).  The host picks the geometry so a tile receives
+//             <= GS/2 positions per sub-chunk on average; a position that would overrun the ring
+//             (or the region capacity) leaves the stream (build: overflow list; probe: tested
+//             against the bitmap in place, a miss clears the key via `neg`).
 //   probe     entry = (j & 3) << 30 | slot << 20 | position-in-tile (slot = thread, j = sub-chunk).
 //             pref[g][q][b] = in-region entries of (g, b) before sub-chunk 4q (b fastest, so a
 //             wave's stores of 64 tiles are one contiguous 256-B run), so k_gather_ring
 //             finds an entry's sub-chunk from its region position and the entry's j & 3.
-//   rounds    The probe runs in two rounds, the batched form of may_contain's early exit
-//             (bloom_filter.py:71-73): round 1 tests seed 0 of every key; round 2 tests seeds
-//             1..k-1 of the keys round 1 left alive (`alive`, the round-1 hit mask), so a
-//             non-member usually costs one position instead of k.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -35,15 +33,18 @@
 namespace pbf {
 
 constexpr uint32_t kRingKeysPerSub = 1024;  // = threads; slot field is 10 bits
-#ifndef PBF_RING_U24
-#define PBF_RING_U24 1
-#endif
+constexpr uint32_t kRingEntries = 32;       // RC: LDS ring entries per tile (64-B groups of 16)
 static_assert(kSlotShift == 20 && kRingKeysPerSub == 1024, "ring entry = (j & 3) << 30 | slot << 20 | position");
-// 2 measured best with the non-temporal streams (C2 A/B over 1/2/3/4/8: profiles/r01/s11/ab.txt)
-#ifndef PBF_RING_PREFETCH
-#define PBF_RING_PREFETCH 2
-#endif
-constexpr int kRingPrefetch = PBF_RING_PREFETCH;  // sub-chunks of keys loaded per batch
+// Key sub-chunks loaded per batch, one batch ahead: 2 measured best with the non-temporal streams
+// (C2 A/B over 1/2/3/4/8: profiles/r01/s11/ab.txt)
+constexpr int kRingPrefetch = 2;
+constexpr uint32_t kRingDescPerWave = 128;  // flush descriptors per wave (64 tiles x <= 2 groups)
+
+// LDS layout of k_part_ring (u32 words): head|tail per tile [B], flush descriptors [16 waves x
+// 128], one dump word (appends that left the stream write there), then the rings [B x RC],
+// 16-B aligned.
+__host__ __device__ constexpr uint32_t ring_lds_base(uint32_t B) { return (B + 16 * kRingDescPerWave + 1 + 3) & ~3u; }
+__host__ __device__ constexpr uint32_t ring_lds_words(uint32_t B) { return ring_lds_base(B) + B * kRingEntries; }
 
 // Tile position of a hash when m is a power of two <= 2^32 (POW2) or in general.
 template <bool POW2>
@@ -56,72 +57,40 @@ __device__ __forceinline__ uint32_t ring_pos(uint32_t h, const TileMap& tm) {
 // counts stores, so the wait for a key load also waits for every flush store issued before it;
 // batching pays that wait once per kRingPrefetch sub-chunks instead of once per sub-chunk.
 // EXACT: k == KMAX is known at compile time, so the per-seed `s < k` tests vanish and the k LDS
-// atomics of a key issue back to back instead of one uniform branch (and one wait) per seed.
-// RCT: the ring size at compile time (0 = pg.ring), so ring addresses, the flush's group count
-// (a division by GS) and its lane split are shifts instead of multiplies and a runtime divide.
-template <int KMAX, int KM, bool PROBE, bool POW2, bool EXACT = false, int RCT = 0>
+// atomics of a key issue back to back.
+// The host keeps cap <= 32768, so a tail never passes cap + one sub-chunk's appends (the flush
+// clamps it every sub-chunk) and head / tail fit the 16-bit halves of one u32: the append is a
+// 32-bit LDS atomic spread over all 32 banks of a lane group.
+template <int KMAX, int KM, bool PROBE, bool POW2, bool EXACT>
 __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k, TileMap tm, PartGeom pg,
                                                     uint32_t* __restrict__ regions, uint32_t* __restrict__ fill,
                                                     uint32_t* __restrict__ pref, uint32_t* __restrict__ ovf,
-                                                    uint32_t* __restrict__ ovf_count,
-                                                    ProbeSet ps, int sbase, const uint32_t* __restrict__ alive,
+                                                    uint32_t* __restrict__ ovf_count, ProbeSet ps,
                                                     uint32_t* __restrict__ hw_init) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     if constexpr (EXACT) k = KMAX;
-    // rings per super-tile of 2^sb tiles (builds of filters with more tiles than the LDS has
-    // rings for; probes: sb = 0, nsup = the tile count)
-    const uint32_t B = pg.nsup;
-    const uint32_t shift = tm.tb + pg.sb;
+    constexpr uint32_t RC = kRingEntries, GS = RC / 2, rmask = RC - 1;
+    const uint32_t B = tm.nbuckets;
+    const uint32_t shift = tm.tb;
     const uint32_t kps = pg.kps;  // keys per sub-chunk (<= 1024 threads)
-    const uint32_t RC = RCT ? uint32_t(RCT) : pg.ring, GS = RC / 2, rmask = RC - 1;
     const uint32_t tid = threadIdx.x, nt = blockDim.x;
     const uint32_t lane = tid & 63, wave = tid >> 6;
     const uint32_t g = blockIdx.x;
     const uint32_t cap = pg.cap;
     const uint32_t lmask = (1u << tm.tb) - 1u;
-    // ht[b] = head << 32 | tail: one 64-bit LDS atomic add appends a position and returns the
-    // tile's flush cursor with its slot (no separate head read per position)
-    unsigned long long* ht = reinterpret_cast<unsigned long long*>(smem);  // B
-    // H32 (the compile-time-ring kernels; the host keeps cap <= 32768 for them): head and tail
-    // as the 16-bit halves of one u32, so the append is a 32-bit atomic spread over all 64 LDS
-    // banks instead of a 64-bit one over 32 bank pairs.  A tail never passes cap + one
-    // sub-chunk's appends (the flush clamps it every sub-chunk), so it stays below 2^16.
-    constexpr bool H32 = RCT != 0;
-    uint32_t* const ht32 = smem;
-    auto ht_get = [&](uint32_t b, uint32_t& h, uint32_t& t) {
-        if constexpr (H32) {
-            const uint32_t v = ht32[b];
-            h = v >> 16;
-            t = v & 0xFFFFu;
-        } else {
-            const unsigned long long v = ht[b];
-            h = uint32_t(v >> 32);
-            t = uint32_t(v);
-        }
-    };
-    auto ht_set = [&](uint32_t b, uint32_t h, uint32_t t) {
-        if constexpr (H32)
-            ht32[b] = (h << 16) | t;
-        else
-            ht[b] = (uint64_t(h) << 32) | t;
-    };
-    uint32_t* desc = smem + 2 * B;                           // 16 waves x 128 group descriptors
-#ifndef PBF_REGION_TILE_MAJOR
-    // this workgroup's regions; an entry's offset in them fits 32 bits (B * cap < 2^32)
+    // ht[b] = head << 16 | tail: one LDS atomic add appends a position and returns the tile's
+    // flush cursor with its slot (no separate head read per position)
+    uint32_t* const ht = smem;
+    uint32_t* const desc = smem + B;                        // 16 waves x 128 group descriptors
+    const uint32_t dump = B + 16 * kRingDescPerWave;  // word index of the dump slot
+    uint32_t* const ring = smem + ring_lds_base(B);          // B * RC, 16-B aligned
+    // this workgroup's regions; an entry's offset in them fits 32 bits (B * cap < 2^32), and
+    // tb < 4096, cap < 2^20 make it one 24-bit multiply-add
     uint32_t* const rgn = regions + uint64_t(g) * B * cap;
-#if PBF_RING_U24
-    // tb < 4096 and cap < 2^20 (plan_for): a 24-bit multiply-add (full rate), not a 64-bit mad
     auto region_at = [&](uint32_t tb, uint32_t e) { return rgn + (__umul24(tb, cap) + e); };
-#else
-    auto region_at = [&](uint32_t tb, uint32_t e) { return rgn + (tb * cap + e); };
-#endif
-#else
-    auto region_at = [&](uint32_t tb, uint32_t e) { return regions + region_id(g, tb, pg.G, B) * cap + e; };
-#endif
-    uint32_t* ring = smem + ((2 * B + 16 * 128 + 3) & ~3u);  // B * RC, 16-B aligned
     const uint32_t nqs = pg.nq + 1;  // pref entries per (g, b)
     for (uint32_t b = tid; b < B; b += nt) {
-        ht_set(b, 0, 0);
+        ht[b] = 0;
         if constexpr (PROBE) pref[uint64_t(g) * nqs * B + b] = 0;
     }
     const uint64_t k0 = uint64_t(g) * pg.kpw;
@@ -140,104 +109,62 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
     constexpr int P = kRingPrefetch;
     constexpr bool F16 = KM == kFixed16;
     uint4 kw[F16 ? P : 1];
-    uint32_t aw[P];  // alive words of this thread's keys (probe round 2)
     auto load_batch = [&](uint64_t c0) {
+        if constexpr (F16) {
 #pragma unroll
-        for (int u = 0; u < P; ++u) {
-            const uint64_t i = c0 + uint64_t(u) * kps + tid;
-            aw[u] = (alive && i < k1) ? alive[i >> 5] : ~0u;
-#ifdef PBF_DIAG_SYNTH_KEYS  // diagnostic (tools/microbench): keys made in registers, no key loads
-            if constexpr (F16) kw[u] = make_uint4(uint32_t(i), uint32_t(i) * 0x9E3779B9u, uint32_t(i >> 7) ^ 0x55u, uint32_t(i) + 17u);
-#else
-            if constexpr (F16) kw[u] = ld_stream_nt<PBF_NT_KEYS != 0>(reinterpret_cast<const uint32_t*>(ks.data) + min(i, n - 1) * 4);
-#endif
+            for (int u = 0; u < P; ++u) {
+                const uint64_t i = c0 + uint64_t(u) * kps + tid;
+                kw[u] = ld_stream_nt<kNtKeys>(reinterpret_cast<const uint32_t*>(ks.data) + min(i, n - 1) * 4);
+            }
         }
     };
     load_batch(k0);
-    PBF_STAMP(7);
     uint32_t j = 0;
     for (uint64_t c0 = k0; c0 < k1; c0 += uint64_t(P) * kps) {
         uint4 cw[F16 ? P : 1];
-        uint32_t ca[P];
+        if constexpr (F16) {
 #pragma unroll
-        for (int u = 0; u < P; ++u) {
-            if constexpr (F16) cw[u] = kw[u];
-            ca[u] = aw[u];
+            for (int u = 0; u < P; ++u) cw[u] = kw[u];
         }
-#ifdef PBF_STAMPS
-        if constexpr (F16) {  // the batch's key-load wait, stamped on its own
-            PBF_STAMP(9);
-            asm volatile("" ::"v"(cw[0].x), "v"(cw[P - 1].w));
-            PBF_STAMP(10);
-        }
-#endif
         if (c0 + uint64_t(P) * kps < k1) load_batch(c0 + uint64_t(P) * kps);
 #pragma unroll
         for (int u = 0; u < P; ++u, ++j) {
             const uint64_t s0 = c0 + uint64_t(u) * kps;
             if (s0 >= k1) break;
             const uint64_t i = s0 + tid;
-            // a probe round after the first hashes only keys that are still possible members
-            const bool live = tid < kps && i < k1 && ((ca[u] >> (i & 31)) & 1u);
+            const bool live = tid < kps && i < k1;
             uint32_t pos[KMAX], slot[KMAX], hd[KMAX];
-            auto hash = [&] {
-                auto emit = [&](int s, uint32_t h) { pos[s] = ring_pos<POW2>(h, tm); };
-                if constexpr (F16)
-                    murmur_seeds16<KMAX>(cw[u], k, emit, sbase);
-                else
-                    hash_key<KMAX, KM>(ks, i, k, emit, sbase);
-            };
-#ifndef PBF_RING_HASH_LATE
             // hash before the barrier: a wave done with its share of the previous flush hashes
             // while the others still flush
-            PBF_STAMP(6);
-            if (live) hash();
-#endif
-            PBF_STAMP(0);
-#ifndef PBF_DIAG_NO_BARRIERS  // diagnostic: with PBF_DIAG_NO_APPEND, the hash and key loads alone
-            lds_barrier();  // previous flush done: head / tail stable, rings free
-#endif
-            PBF_STAMP(1);
-#ifdef PBF_RING_HASH_LATE
-            if (live) hash();
-#endif
-#ifdef PBF_DIAG_NO_APPEND  // diagnostic (tools/microbench): positions hashed, not appended
             if (live) {
-                uint32_t x = 0;
-#pragma unroll
-                for (int s = 0; s < KMAX; ++s)
-                    if (s < k) x ^= pos[s];
-                if (x == 0x9E3779B9u) fill[0] = x;  // keeps the hash live
+                auto emit = [&](int s, uint32_t h) { pos[s] = ring_pos<POW2>(h, tm); };
+                if constexpr (F16)
+                    murmur_seeds16<KMAX>(cw[u], k, emit);
+                else
+                    hash_key<KMAX, KM>(ks, i, k, emit);
             }
-            if (false) {
-#else
+            lds_barrier();  // previous flush done: head / tail stable, rings free
             if (live) {
-#endif
 #pragma unroll
                 for (int s = 0; s < KMAX; ++s) {
                     if (s < k) {
-                        if constexpr (H32) {
-                            const uint32_t v = atomicAdd(ht32 + (pos[s] >> shift), 1u);
-                            slot[s] = v & 0xFFFFu;
-                            hd[s] = v >> 16;
-                        } else {
-                            const unsigned long long v = atomicAdd(ht + (pos[s] >> shift), 1ull);
-                            slot[s] = uint32_t(v);
-                            hd[s] = uint32_t(v >> 32);
-                        }
+                        const uint32_t v = atomicAdd(ht + (pos[s] >> shift), 1u);
+                        slot[s] = v & 0xFFFFu;
+                        hd[s] = v >> 16;
                     }
                 }
-                PBF_STAMP(2);
                 uint32_t spill = 0;  // positions that overrun their tile's ring or region
+                const uint32_t tag = PROBE ? (((j & 3u) << 30) | (tid << kSlotShift)) : 0u;
 #pragma unroll
                 for (int s = 0; s < KMAX; ++s) {
                     if (s < k) {
                         const uint32_t p = pos[s], b = p >> shift, e = slot[s];
-                        if (e - hd[s] < RC && e < cap)
-                            ring[b * RC + (e & rmask)] =
-                                PROBE ? (((j & 3u) << 30) | (tid << kSlotShift) | (p & lmask)) : p;
-                        else
-                            spill |= 1u << s;
+                        const bool ok = e - hd[s] < RC && e < cap;
+                        const uint32_t val = PROBE ? (tag | (p & lmask)) : p;
+                        // every lane stores (a position that left the stream into the dump
+                        // word): no per-seed exec-mask branch (build 0.196 -> 0.192 ms on C2)
+                        smem[ok ? ring_lds_base(B) + b * RC + (e & rmask) : dump] = val;
+                        spill |= uint32_t(!ok) << s;
                     }
                 }
                 if (spill) {  // rare (heavy key duplication): out of the stream
@@ -253,25 +180,20 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
                     }
                 }
             }
-            PBF_STAMP(3);
-#ifdef PBF_DIAG_NO_BARRIERS
-            continue;
-#endif
             lds_barrier();
-            PBF_STAMP(4);
             // Flush: each wave owns 64 tiles per pass.  A lane's tile has 0..2 whole groups;
             // the wave lists them (descriptor = tile | region position << 12) and writes
             // 64/(GS/4) groups per store instruction, GS/4 lanes x 16 B per group, each whole.
-            uint32_t* wd = desc + wave * 128;
-            const uint32_t lpg = GS / 4;    // lanes per group
-            const uint32_t gpi = 64 / lpg;  // groups per store instruction
+            uint32_t* wd = desc + wave * kRingDescPerWave;
+            constexpr uint32_t lpg = GS / 4;    // lanes per group
+            constexpr uint32_t gpi = 64 / lpg;  // groups per store instruction
             for (uint32_t b0 = wave * 64; b0 < B; b0 += nt) {
                 const uint32_t b = b0 + lane;
                 uint32_t ng = 0, h = 0, t = 0;
                 if (b < B) {
-                    uint32_t tail;
-                    ht_get(b, h, tail);
-                    t = min(tail, min(h + RC, cap));  // positions past these left the stream
+                    const uint32_t v = ht[b];
+                    h = v >> 16;
+                    t = min(v & 0xFFFFu, min(h + RC, cap));  // positions past these left the stream
                     ng = (t - h) / GS;
                 }
                 const uint64_t m1 = __ballot(ng >= 1), m2 = __ballot(ng >= 2);
@@ -291,33 +213,32 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
                         const uint32_t tb = d & 0xFFFu;
                         const uint32_t e = (d >> 12) + q * 4;  // region position
                         const uint4 v = *reinterpret_cast<const uint4*>(ring + tb * RC + (e & rmask));
-#ifdef PBF_DIAG_NO_STORES  // diagnostic (tools/microbench): the flush's group stores left out
-                        if (v.x == 0xFFFFFFFFu && v.y == 0xFFFFFFFFu && v.z == 0xFFFFFFFFu && v.w == 0xFFFFFFFFu)
-#endif
-                        st_stream<(PBF_NT_STORE & (PROBE ? 2 : 1)) != 0>(region_at(tb, e), v);
+                        st_stream<PROBE ? kNtProbePart : kNtBuildPart>(region_at(tb, e), v);
                     }
                 }
                 __builtin_amdgcn_wave_barrier();
                 if (b < B) {
-                    ht_set(b, h + ng * GS, t);
+                    ht[b] = ((h + ng * GS) << 16) | t;
                     if constexpr (PROBE)
                         if (((j + 1) & 3) == 0) pref[(uint64_t(g) * nqs + ((j + 1) >> 2)) * B + b] = t;
                 }
             }
-            PBF_STAMP(5);
         }
     }
-    PBF_STAMP(8);
     lds_barrier();
     // The last partial group of every tile leaves as a whole group too (entries past the fill
     // count are never read; the region has room: head is a multiple of GS and cap of 32).
     {
-        uint32_t* wd = desc + wave * 128;
-        const uint32_t lpg = GS / 4, gpi = 64 / lpg;
+        uint32_t* wd = desc + wave * kRingDescPerWave;
+        constexpr uint32_t lpg = GS / 4, gpi = 64 / lpg;
         for (uint32_t b0 = wave * 64; b0 < B; b0 += nt) {
             const uint32_t b = b0 + lane;
             uint32_t hh = 0, tt = 0;
-            if (b < B) ht_get(b, hh, tt);
+            if (b < B) {
+                const uint32_t v = ht[b];
+                hh = v >> 16;
+                tt = v & 0xFFFFu;
+            }
             const bool part = tt > hh;
             const uint64_t m1 = __ballot(part);
             const uint32_t at = __popcll(m1 & ((uint64_t(1) << lane) - 1)), total = __popcll(m1);
@@ -330,7 +251,7 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
                     const uint32_t tb = d & 0xFFFu;
                     const uint32_t e = (d >> 12) + q * 4;
                     const uint4 v = *reinterpret_cast<const uint4*>(ring + tb * RC + (e & rmask));
-                    st_stream<(PBF_NT_STORE & (PROBE ? 2 : 1)) != 0>(region_at(tb, e), v);
+                    st_stream<PROBE ? kNtProbePart : kNtBuildPart>(region_at(tb, e), v);
                 }
             }
             __builtin_amdgcn_wave_barrier();
@@ -338,8 +259,7 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
     }
     // fill counts; the probe's remaining cumulative counts
     for (uint32_t b = tid; b < B; b += nt) {
-        uint32_t hh, t;
-        ht_get(b, hh, t);
+        const uint32_t t = ht[b] & 0xFFFFu;
         fill[uint64_t(b) * pg.G + g] = t;
         if constexpr (PROBE)
             for (uint32_t q = (j + 3) >> 2; q <= pg.nq; ++q) pref[(uint64_t(g) * nqs + q) * B + b] = t;
@@ -366,15 +286,14 @@ __global__ void __launch_bounds__(512) k_gather_ring(TileMap tm, PartGeom pg, ui
                                                      const uint32_t* __restrict__ regions,
                                                      const uint32_t* __restrict__ R, const uint32_t* __restrict__ fill,
                                                      const uint32_t* __restrict__ pref,
-                                                     const uint32_t* __restrict__ neg, const uint32_t* __restrict__ alive,
-                                                     uint8_t* __restrict__ hitmask, uint32_t* __restrict__ hw,
-                                                     uint32_t nf, uint64_t r_stride, uint64_t neg_stride, uint32_t tq,
-                                                     int packed) {
+                                                     const uint32_t* __restrict__ neg, uint8_t* __restrict__ hitmask,
+                                                     uint32_t* __restrict__ hw, uint32_t nf, uint64_t r_stride,
+                                                     uint64_t neg_stride, uint32_t tq) {
     extern __shared__ uint32_t smem[];
     if constexpr (NFM == 1) nf = 1;
     const uint32_t B = tm.nbuckets, cap = pg.cap, wpr = cap / 32, nqs = pg.nq + 1;
     const uint32_t tid = threadIdx.x, nt = blockDim.x;
-    const uint32_t lane = tid & 63, wave = tid >> 6, nwaves = nt >> 6;
+    const uint32_t wave = tid >> 6, nwaves = nt >> 6, lane = tid & 63;
     const uint32_t g = blockIdx.x;
     const uint32_t S = gridDim.y, sp = blockIdx.y;
     const uint32_t b_lo = uint32_t(uint64_t(B) * sp / S), b_hi = uint32_t(uint64_t(B) * (sp + 1) / S);
@@ -387,18 +306,11 @@ __global__ void __launch_bounds__(512) k_gather_ring(TileMap tm, PartGeom pg, ui
     uint16_t* lpref = reinterpret_cast<uint16_t*>(kbits + nf * kw);  // nb * nqs (values <= cap < 2^16)
     uint8_t* qtab = reinterpret_cast<uint8_t*>(lpref + ((nb * nqs + 1) & ~1u));  // nb * tq (tq > 0)
     const uint32_t* gp = pref + uint64_t(g) * nqs * B;  // [q][b] in memory, [b][q] in LDS
-#ifndef PBF_REGION_TILE_MAJOR
     // workgroup g's regions and result words; offsets within them fit 32 bits (B * cap < 2^32)
     const uint32_t* const rgn = regions + uint64_t(g) * B * cap;
     const uint32_t* const Rg = R + uint64_t(g) * B * wpr;
     auto entries_at = [&](uint32_t b, uint32_t r) { return rgn + (b * cap + r); };
     auto rword = [&](uint32_t f, uint32_t b, uint32_t r) { return Rg[f * r_stride + (b * wpr + (r >> 5))]; };
-#else
-    auto entries_at = [&](uint32_t b, uint32_t r) { return regions + region_id(g, b, pg.G, B) * cap + r; };
-    auto rword = [&](uint32_t f, uint32_t b, uint32_t r) {
-        return R[f * r_stride + region_id(g, b, pg.G, B) * wpr + (r >> 5)];
-    };
-#endif
     for (uint32_t x = tid; x < nb * nqs; x += nt) {
         const uint32_t q = x / nb, bb = x - q * nb;
         lpref[bb * nqs + q] = uint16_t(gp[uint64_t(q) * B + b_lo + bb]);
@@ -419,111 +331,13 @@ __global__ void __launch_bounds__(512) k_gather_ring(TileMap tm, PartGeom pg, ui
         for (uint32_t w = tid; w < kw; w += nt) {
             const uint32_t key0 = w * 32;
             uint32_t m = key0 >= nkeys ? 0u : (nkeys - key0 >= 32 ? ~0u : ((1u << (nkeys - key0)) - 1u));
-            if (m) {  // k0 is a multiple of 64
-                m &= ~neg[f * neg_stride + ((k0 + key0) >> 5)];
-                if (alive) m &= alive[(k0 + key0) >> 5];  // refuted by an earlier probe round
-            }
+            if (m) m &= ~neg[f * neg_stride + ((k0 + key0) >> 5)];  // k0 is a multiple of 64
             kbits[f * kw + w] = m;
         }
     }
     lds_barrier();
-    if (packed) {
-        // The split's regions as ONE list of 4-entry quads: rq[bb] = quads of regions before bb
-        // (exclusive prefix of ceil(fill / 4), fill = the row's last pref).  Every load round
-        // then serves 64 quads per wave instruction, however the fills fall, instead of up to
-        // three rounds per region whose last one has few lanes.
-        uint32_t* rq = reinterpret_cast<uint32_t*>(qtab + ((nb * (tq ? tq : 0) + 3) & ~3u));
-        if (wave == 0) {
-            uint32_t carry = 0;
-            for (uint32_t c0 = 0; c0 < nb; c0 += 64) {
-                const uint32_t bb = c0 + lane;
-                uint32_t v = bb < nb ? (uint32_t(lpref[bb * nqs + nqs - 1]) + 3) >> 2 : 0u;
-#pragma unroll
-                for (int d = 1; d < 64; d <<= 1) {
-                    const uint32_t o = __shfl_up(v, d, 64);
-                    if (lane >= uint32_t(d)) v += o;
-                }
-                if (bb < nb) rq[bb + 1] = carry + v;  // inclusive -> exclusive of bb + 1
-                carry += __shfl(v, 63, 64);
-            }
-            if (lane == 0) rq[0] = 0;
-        }
-        lds_barrier();
-        const uint32_t T = rq[nb];
-        constexpr int UP = 4;
-        for (uint32_t base = wave * 64; base < T; base += nwaves * 64 * UP) {
-            uint4 v[UP];
-            uint32_t rw[NFM][UP], bq[UP], rr[UP];
-#pragma unroll
-            for (int u = 0; u < UP; ++u) {
-                const uint32_t s0 = min(base + uint32_t(u) * nwaves * 64, T - 1);
-                const uint32_t qi = min(s0 + lane, T - 1);
-                // the wave's first quad's region (uniform binary search), then each lane steps
-                // over the few region ends among its wave's 64 quads
-                uint32_t lo = 0, len = nb + 1;
-                while (len > 1) {
-                    const uint32_t half = len >> 1;
-                    if (rq[lo + half] <= s0) lo += half;
-                    len -= half;
-                }
-                while (lo + 1 < nb && rq[lo + 1] <= qi) ++lo;
-                bq[u] = lo;
-                rr[u] = (qi - rq[lo]) * 4;
-                v[u] = ld_stream(entries_at(b_lo + lo, rr[u]));
-#pragma unroll
-                for (int f = 0; f < NFM; ++f)
-                    if (uint32_t(f) < nf) rw[f][u] = rword(f, b_lo + lo, rr[u]);
-            }
-#pragma unroll
-            for (int u = 0; u < UP; ++u) {
-                const uint32_t qi = base + uint32_t(u) * nwaves * 64 + lane;
-                if (qi >= T) continue;
-                const uint32_t bb = bq[u], r = rr[u];
-                const uint16_t* pb = lpref + bb * nqs;
-                const uint32_t fillr = pb[nqs - 1];
-                const uint32_t lim = fillr - r < 4 ? (1u << (fillr - r)) - 1u : 0xFu;
-                uint32_t fl[NFM], any = 0;
-#pragma unroll
-                for (int f = 0; f < NFM; ++f) {
-                    fl[f] = uint32_t(f) < nf ? (~r_quad(rw[f][u], r) & lim) : 0u;
-                    any |= fl[f];
-                }
-                if (!any) continue;
-                uint32_t lo = 0;
-                if (tq) {
-                    lo = qtab[bb * tq + (r >> 2)];
-                } else {
-                    uint32_t len = nqs;
-                    while (len > 1) {
-                        const uint32_t half = len >> 1;
-                        if (pb[lo + half] <= r) lo += half;
-                        len -= half;
-                    }
-                }
-                const uint32_t vv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-                // the next group's first entry: a boundary inside the quad is rare (a group
-                // holds ~24 entries at C2), so entries usually take lo with one compare
-                uint32_t nxt = lo + 1 < nqs ? uint32_t(pb[lo + 1]) : 0xFFFFFFFFu;
-#pragma unroll
-                for (int t = 0; t < 4; ++t) {
-                    if ((any >> t) & 1u) {
-                        if (r + t >= nxt) {
-                            ++lo;
-                            while (lo + 1 < nqs && pb[lo + 1] <= r + t) ++lo;
-                            nxt = lo + 1 < nqs ? uint32_t(pb[lo + 1]) : 0xFFFFFFFFu;
-                        }
-                        // key = (4 lo + (j & 3)) * 1024 + slot = lo << 12 | the entry's top 12 bits
-                        const uint32_t key = (lo << 12) + (vv[t] >> kSlotShift);
-#pragma unroll
-                        for (int f = 0; f < NFM; ++f)
-                            if ((fl[f] >> t) & 1u) atomicAnd(kbits + f * kw + (key >> 5), ~(1u << (key & 31)));
-                    }
-                }
-            }
-        }
-    }
-    constexpr int U = PBF_GATHER_U;  // regions in flight per wave
-    for (uint32_t b0 = b_lo + wave; !packed && b0 < b_hi; b0 += nwaves * U) {
+    constexpr int U = kGatherRegionsInFlight;
+    for (uint32_t b0 = b_lo + wave; b0 < b_hi; b0 += nwaves * U) {
         uint32_t fillb[U];
 #pragma unroll
         for (int u = 0; u < U; ++u)
@@ -536,10 +350,11 @@ __global__ void __launch_bounds__(512) k_gather_ring(TileMap tm, PartGeom pg, ui
             uint32_t rw[NFM][U];
             // single filter: result words first; a quad's entries (only their key ids are
             // needed) are loaded only when one of its entries failed, so quads that passed (a
-            // probe batch's members) cost their result bits alone.  Multi-filter sets: nearly
-            // every quad fails some filter, so entries and result words go out together.
+            // probe batch's members) cost their result bits alone (C2 probe 0.517 -> 0.504 ms).
+            // Multi-filter sets: nearly every quad fails some filter, so entries and result
+            // words go out together.
             uint32_t anyq[U];  // one filter: the quad's failed entries as byte-spread bits (0: skip)
-            if constexpr (PBF_GATHER_RFIRST && NFM == 1) {
+            if constexpr (NFM == 1) {
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
                     const uint32_t b = min(b0 + u * nwaves, b_hi - 1);

@@ -35,17 +35,23 @@
 namespace pbf {
 
 // Streaming access to the region entries and the bitmap tile write-out: each byte is written
-// once and read back once or twice by a later kernel, far beyond L2. PBF_NT_LOAD marks the
-// region-entry loads non-temporal; PBF_NT_STORE is a bit set — 1: build partition stores,
-// 2: probe partition stores, 4: k_tile_build's bitmap write-out. Defaults = the best of the A/B
-// builds on C2 (profiles/r01/s9/nt_ab.txt): loads + probe partition + bitmap write-out
-// (0.886 -> 0.822 ms/step); non-temporal build-partition stores measured slower (+10 us).
-#ifndef PBF_NT_STORE
-#define PBF_NT_STORE 6
-#endif
-#ifndef PBF_NT_LOAD
-#define PBF_NT_LOAD 1
-#endif
+// once and read back once or twice by a later kernel, far beyond L2, so those accesses are
+// non-temporal.  Choices are the best of the A/B builds on C2 (profiles/r01/s9/nt_ab.txt,
+// profiles/r01/s10/nt_ab.txt): region-entry loads, probe-partition stores, the tile build's
+// bitmap write-out and the partition's 16-B key loads non-temporal (0.886 -> 0.801 ms/step);
+// non-temporal build-partition stores measured 10 us slower, non-temporal bitmap loads into the
+// LDS tiles no gain.
+constexpr bool kNtLoad = true;        // region entries
+constexpr bool kNtBuildPart = false;  // build partition's group stores
+constexpr bool kNtProbePart = true;   // probe partition's group stores
+constexpr bool kNtTileStore = true;   // k_tile_build's bitmap write-out
+constexpr bool kNtKeys = true;        // the partitions' 16-B key loads
+constexpr bool kNtTileLoad = false;   // bitmap loads into the LDS tiles
+// Regions of loads in flight per wave: the tile build 4, the tile test 8 words, the gather 4
+// (16 loads per wave in the tile test and 8 regions in the gather measured slower).
+constexpr int kTileBuildRegionsInFlight = 4;
+constexpr int kTileProbeWordsInFlight = 8;
+constexpr int kGatherRegionsInFlight = 4;
 typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
 
 template <bool NT>
@@ -68,28 +74,7 @@ __device__ __forceinline__ uint4 ld_stream_nt(const uint32_t* p) {
     }
 }
 
-// The partition's 16-B key loads (each key is read once per pass): non-temporal, 0.819 ->
-// 0.801 ms/step on C2. The tile passes' bitmap loads (PBF_NT_TILE) measured no gain: off.
-// A/B records: profiles/r01/s10/nt_ab.txt.
-#ifndef PBF_NT_KEYS
-#define PBF_NT_KEYS 1
-#endif
-#ifndef PBF_NT_TILE
-#define PBF_NT_TILE 0
-#endif
-// gathers read a region quad's entries only when one of its result bits failed (the ring
-// gather of one filter: C2 probe 0.517 -> 0.504 ms; the counting-sort gather: neutral on C3, off)
-#ifndef PBF_GATHER_RFIRST
-#define PBF_GATHER_RFIRST 1
-#endif
-#ifndef PBF_GATHER_U
-#define PBF_GATHER_U 4
-#endif
-#ifndef PBF_GATHER_RFIRST_SORT
-#define PBF_GATHER_RFIRST_SORT 0
-#endif
-
-__device__ __forceinline__ uint4 ld_stream(const uint32_t* p) { return ld_stream_nt<PBF_NT_LOAD != 0>(p); }
+__device__ __forceinline__ uint4 ld_stream(const uint32_t* p) { return ld_stream_nt<kNtLoad>(p); }
 
 struct TileMap {
     IndexMap im;
@@ -120,15 +105,10 @@ __device__ __forceinline__ void spill_probe(const ProbeSet& ps, uint64_t bit, ui
             atomicOr(ps.neg + f * ps.neg_stride + (key >> 5), 1u << (key & 31));
 }
 
-// Region (g, b) = partition workgroup g's entries of tile b.  PBF_REGION_TILE_MAJOR lays the
-// regions out tile-major (a tile's G regions back to back: contiguous for the tile passes) instead
-// of workgroup-major (a workgroup's B regions back to back: contiguous for the gather).
-__device__ __forceinline__ uint64_t region_id(uint32_t g, uint32_t b, uint32_t G, uint32_t B) {
-#ifdef PBF_REGION_TILE_MAJOR
-    return uint64_t(b) * G + g;
-#else
+// Region (g, b) = partition workgroup g's entries of tile b, workgroup-major (a workgroup's B
+// regions back to back: contiguous for the gather; tile-major measured no different).
+__device__ __forceinline__ uint64_t region_id(uint32_t g, uint32_t b, uint32_t /*G*/, uint32_t B) {
     return uint64_t(g) * B + b;
-#endif
 }
 
 struct PartGeom {
@@ -139,8 +119,6 @@ struct PartGeom {
     uint64_t kpw;      // keys per workgroup (= nsub * kps)
     uint32_t nq;       // ring partition: pref groups (4 sub-chunks each) per workgroup
     uint32_t ring;     // ring partition: LDS ring entries per tile (0 = counting-sort partition)
-    uint32_t sb;       // ring build: log2 tiles per super-tile (regions are per super-tile)
-    uint32_t nsup;     // ring partition: super-tiles (= tiles when sb = 0)
 };
 
 constexpr uint32_t kSlotShift = 20;   // probe entry = slot-in-sub-chunk << 20 | position in tile
@@ -162,22 +140,6 @@ __device__ __forceinline__ uint64_t tile_word0(uint32_t t, const TileMap& tm) {
     if (tm.cspace && p0 >= (1ull << 31)) w += tm.delta_words;
     return w;
 }
-
-// Diagnostic phase stamps (tools/microbench/part_phases.hip builds with PBF_STAMPS; the product
-// build compiles them away).  Workgroup 0, wave 0, lane 0 records s_memtime per phase.
-#ifdef PBF_STAMPS
-__device__ unsigned long long* g_stamps;
-#define PBF_STAMP(slot)                                                                         \
-    do {                                                                                        \
-        __builtin_amdgcn_sched_barrier(0);                                                      \
-        unsigned long long t_;                                                                  \
-        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");              \
-        if (blockIdx.x == 0 && threadIdx.x == 0) g_stamps[(slot)] += t_;                        \
-        __builtin_amdgcn_sched_barrier(0);                                                      \
-    } while (0)
-#else
-#define PBF_STAMP(slot) do {} while (0)
-#endif
 
 // Barrier for LDS hand-offs only: waits for this wave's LDS/scalar operations, not for its
 // global stores (which __syncthreads' workgroup-release fence would drain every time).
@@ -282,7 +244,7 @@ __global__ void __launch_bounds__(kPartThreads) k_part(KeySet ks, uint64_t n, in
 #pragma unroll
             for (int u = 0; u < KPT; ++u) {
                 const uint64_t i = min(s0 + u * nt + tid, n - 1);
-                kw[u] = ld_stream_nt<PBF_NT_KEYS != 0>(reinterpret_cast<const uint32_t*>(ks.data) + i * 4);
+                kw[u] = ld_stream_nt<kNtKeys>(reinterpret_cast<const uint32_t*>(ks.data) + i * 4);
             }
         }
     };
@@ -290,10 +252,8 @@ __global__ void __launch_bounds__(kPartThreads) k_part(KeySet ks, uint64_t n, in
     uint32_t j = 0;
     for (uint64_t s0 = k0; s0 < k1; s0 += pg.kps, ++j) {
         const uint64_t s1 = min(k1, s0 + pg.kps);
-        PBF_STAMP(0);
         for (uint32_t b = tid; b < B; b += nt) cnt[b] = 0;
         lds_barrier();
-        PBF_STAMP(1);
         // (initialised so no value stays live across the sub-chunk loop's back-edge)
         uint32_t pos[KPT * KMAX], rk[KPT * KMAX];
 #pragma unroll
@@ -313,15 +273,12 @@ __global__ void __launch_bounds__(kPartThreads) k_part(KeySet ks, uint64_t n, in
                     hash_key<KMAX, KM>(ks, i, k, emit);
             }
         }
-        PBF_STAMP(2);
         lds_barrier();
-        PBF_STAMP(3);
         if constexpr (PROBE) {
             uint32_t* sc = subcnt + (uint64_t(g) * pg.nsub + j) * B;
             for (uint32_t b = tid; b < B; b += nt) sc[b] = cnt[b];
         }
         block_exclusive_scan(cnt, lbase, B, ws);
-        PBF_STAMP(4);
 #pragma unroll
         for (int u = 0; u < KPT; ++u) {
             const uint32_t slot_key = u * nt + tid;
@@ -339,7 +296,6 @@ __global__ void __launch_bounds__(kPartThreads) k_part(KeySet ks, uint64_t n, in
         }
         for (uint32_t b = tid; b < B; b += nt) cursor[b] -= lbase[b];
         lds_barrier();
-        PBF_STAMP(5);
         if (s0 + pg.kps < k1) load_keys(s0 + pg.kps);
         // Lane-parallel write-out: entry e of the sorted stage goes to position
         // cursor[b] + (e - lbase[b]) of region (g, b) (cursor pre-biased by -lbase below).
@@ -372,7 +328,6 @@ __global__ void __launch_bounds__(kPartThreads) k_part(KeySet ks, uint64_t n, in
         }
         lds_barrier();
         for (uint32_t b = tid; b < B; b += nt) cursor[b] += lbase[b + 1];
-        PBF_STAMP(6);
     }
     lds_barrier();
     for (uint32_t b = tid; b < B; b += nt) {
@@ -394,7 +349,7 @@ __device__ __forceinline__ void load_tile(uint32_t* tile, const uint32_t* __rest
         for (uint32_t q0 = tid; q0 < W4; q0 += nt * 8) {
             uint4 v[8];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) v[u] = ld_stream_nt<PBF_NT_TILE != 0>(reinterpret_cast<const uint32_t*>(src + min(q0 + u * nt, W4 - 1)));
+            for (int u = 0; u < 8; ++u) v[u] = ld_stream_nt<kNtTileLoad>(reinterpret_cast<const uint32_t*>(src + min(q0 + u * nt, W4 - 1)));
 #pragma unroll
             for (int u = 0; u < 8; ++u)
                 if (q0 + u * nt < W4) reinterpret_cast<uint4*>(tile)[q0 + u * nt] = v[u];
@@ -409,50 +364,35 @@ __device__ __forceinline__ void store_tile(const uint32_t* tile, uint32_t* __res
     const uint32_t tid = threadIdx.x, nt = blockDim.x;
     if ((w0 & 3) == 0 && (nw & 3) == 0) {
         uint4* dst = reinterpret_cast<uint4*>(bitmap + w0);
-        for (uint32_t q = tid; q < nw / 4; q += nt) st_stream<(PBF_NT_STORE & 4) != 0>(reinterpret_cast<uint32_t*>(dst + q), reinterpret_cast<const uint4*>(tile)[q]);
+        for (uint32_t q = tid; q < nw / 4; q += nt) st_stream<kNtTileStore>(reinterpret_cast<uint32_t*>(dst + q), reinterpret_cast<const uint4*>(tile)[q]);
     } else {
         for (uint32_t w = tid; w < nw; w += nt) bitmap[w0 + w] = tile[w];
     }
 }
 
-// OR the in-fill entries of a 4-entry piece into the LDS tile.  SUPER: the region holds a whole
-// super-tile's positions; only those of this workgroup's tile t (p >> tb == t) are taken.
-template <bool SUPER = false>
-__device__ __forceinline__ void or_bits4(uint32_t* tile, uint4 v, uint32_t e, uint32_t f, uint32_t lmask,
-                                         uint32_t tb = 0, uint32_t t = 0) {
+// OR the in-fill entries of a 4-entry piece into the LDS tile.
+__device__ __forceinline__ void or_bits4(uint32_t* tile, uint4 v, uint32_t e, uint32_t f, uint32_t lmask) {
     const uint32_t vv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         const uint32_t p = vv[q] & lmask;
-        if (e + q < f && (!SUPER || (vv[q] >> tb) == t)) atomicOr(tile + (p >> 5), 1u << (p & 31));
+        if (e + q < f) atomicOr(tile + (p >> 5), 1u << (p & 31));
     }
 }
 
 // ------------------------------------------------------------------ build: tiles
 // One workgroup per tile.  A wave (64 lanes x 16-byte loads = 256 entries) covers one region
-// per step and keeps U regions of loads in flight.
-// SUPER (ring build with 2^sb tiles per super-tile): workgroup (super-tile s, part h) builds
-// tile t = s * 2^sb + h from the regions of s.  The 2^sb workgroups of one super-tile are dealt
-// onto one XCD and dispatched together (block x = ((s / 8) * 2^sb + h) * 8 + s % 8; round-robin
-// XCD placement, speed only), so they stream the same region entries and all but the first
-// read them from that XCD's L2.
-template <bool SUPER>
+// per step and keeps kTileBuildRegionsInFlight regions of loads in flight.
 __global__ void __launch_bounds__(1024) k_tile_build(TileMap tm, PartGeom pg, const uint32_t* __restrict__ regions,
                                                      const uint32_t* __restrict__ fill, uint32_t* __restrict__ bitmap,
                                                      int pristine) {
     extern __shared__ uint32_t smem[];
-    const uint32_t B = pg.nsup, G = pg.G, cap = pg.cap;
-    uint32_t b = blockIdx.x, t = blockIdx.x;  // region column (super-tile) and the tile built
-    if constexpr (SUPER) {
-        const uint32_t x = blockIdx.x, parts = 1u << pg.sb, q = x >> 3;
-        b = (q >> pg.sb) * 8 + (x & 7);
-        t = (b << pg.sb) + (q & (parts - 1));
-        if (b >= pg.nsup || t >= tm.nbuckets) return;
-    }
+    const uint32_t B = tm.nbuckets, G = pg.G, cap = pg.cap;
+    const uint32_t b = blockIdx.x;
     const uint32_t W = 1u << (tm.tb - 5);
     uint32_t* tile = smem;       // W
     uint32_t* fills = tile + W;  // G
-    const uint64_t w0 = tile_word0(t, tm);
+    const uint64_t w0 = tile_word0(b, tm);
     const uint32_t nw = uint32_t(min<uint64_t>(W, tm.total_words - w0));
     const uint32_t tid = threadIdx.x, nt = blockDim.x;
     for (uint32_t q = tid; q < G; q += nt) fills[q] = fill[uint64_t(b) * G + q];
@@ -464,10 +404,7 @@ __global__ void __launch_bounds__(1024) k_tile_build(TileMap tm, PartGeom pg, co
     lds_barrier();
     const uint32_t lane = tid & 63, wave = tid >> 6, nwaves = nt >> 6;
     const uint32_t lmask = (1u << tm.tb) - 1u;
-#ifndef PBF_TB_U
-#define PBF_TB_U 4
-#endif
-    constexpr int U = PBF_TB_U;  // regions of loads in flight per wave
+    constexpr int U = kTileBuildRegionsInFlight;
     for (uint32_t g0 = wave; g0 < G; g0 += nwaves * U) {
         uint4 v[U];
         uint32_t f[U];
@@ -477,20 +414,18 @@ __global__ void __launch_bounds__(1024) k_tile_build(TileMap tm, PartGeom pg, co
             f[u] = q < G ? fills[q] : 0u;
             // unconditional loads, clamped to the filled part (idle lanes re-read its last line)
             const uint32_t lc = min(lane, (max(f[u], 1u) - 1) >> 2);
-            // siblings of a super-tile read these lines too: keep them in L2 (temporal loads)
-            v[u] = ld_stream_nt<!SUPER && PBF_NT_LOAD != 0>(regions + region_id(min(q, G - 1), b, G, B) * cap + lc * 4);
+            v[u] = ld_stream_nt<kNtLoad>(regions + region_id(min(q, G - 1), b, G, B) * cap + lc * 4);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u)
-            if (lane * 4 < f[u]) or_bits4<SUPER>(tile, v[u], lane * 4, f[u], lmask, tm.tb, t);
+            if (lane * 4 < f[u]) or_bits4(tile, v[u], lane * 4, f[u], lmask);
     }
     // regions holding more than 256 entries
     if (cap > 256) {
         for (uint32_t q = wave; q < G; q += nwaves) {
             const uint32_t fq = fills[q];
             for (uint32_t c = 64 + lane; c * 4 < fq; c += 64)
-                or_bits4<SUPER>(tile, ld_stream_nt<!SUPER && PBF_NT_LOAD != 0>(regions + region_id(q, b, G, B) * cap + c * 4),
-                                c * 4, fq, lmask, tm.tb, t);
+                or_bits4(tile, ld_stream_nt<kNtLoad>(regions + region_id(q, b, G, B) * cap + c * 4), c * 4, fq, lmask);
         }
     }
     lds_barrier();
@@ -568,10 +503,7 @@ __device__ __forceinline__ void tile_probe_body(uint32_t* smem, uint32_t b, cons
     const uint32_t lane = tid & 63, wave = tid >> 6, nwaves = nt >> 6;
     const uint32_t l = lane & 7, wsub = lane >> 3;  // piece of the word, word of the instruction
     const uint32_t stride = nwaves * 8;
-#ifndef PBF_TP_U
-#define PBF_TP_U 8
-#endif
-    constexpr int U = PBF_TP_U;  // instructions (8 words each) in flight per wave
+    constexpr int U = kTileProbeWordsInFlight;  // instructions (8 words each) in flight per wave
     for (uint32_t c0 = wave * 8; c0 < total; c0 += stride * U) {
         uint4 v[U];
         uint32_t oo[U], lim[U];
@@ -619,7 +551,7 @@ __global__ void __launch_bounds__(1024) k_tile_probe(TileMap tm, PartGeom pg, co
                                                      const uint32_t* __restrict__ fill,
                                                      const uint32_t* __restrict__ bitmap, uint32_t* __restrict__ R) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-    tile_probe_body<PBF_NT_LOAD != 0, EXPAND>(smem, blockIdx.x, tm, pg, regions, fill, bitmap, R);
+    tile_probe_body<kNtLoad, EXPAND>(smem, blockIdx.x, tm, pg, regions, fill, bitmap, R);
 }
 
 // The tile test of a multi-filter probe in ONE launch: workgroup (tile b, filter f) for every
@@ -715,24 +647,9 @@ __global__ void __launch_bounds__(512) k_gather(TileMap tm, PartGeom pg, uint64_
                 const uint32_t b = min(b0 + u * nwaves, b_hi - 1);
                 const uint32_t r = min(r0 + lane * 4, (max(fillb[u], 1u) - 1) & ~3u);
                 const uint64_t reg = region_id(g, b, pg.G, B);
-#if !PBF_GATHER_RFIRST_SORT
                 v[u] = ld_stream(regions + reg * cap + r);
-#endif
                 rw[u] = R[reg * wpr + (r >> 5)];
             }
-#if PBF_GATHER_RFIRST_SORT
-            // entries (for their key ids) only of quads with a failed result bit
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const uint32_t b = b0 + u * nwaves;
-                const uint32_t r = r0 + lane * 4;
-                if (b < b_hi && r < fillb[u]) {
-                    uint32_t fails = ~r_quad(rw[u], r) & 0xFu;
-                    if (fillb[u] - r < 4) fails &= (1u << (fillb[u] - r)) - 1u;
-                    if (fails) v[u] = ld_stream(regions + region_id(g, b, pg.G, B) * cap + r);
-                }
-            }
-#endif
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const uint32_t b = b0 + u * nwaves;

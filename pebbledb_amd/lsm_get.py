@@ -16,6 +16,11 @@ SSTable, numbered L0 first then level by level (``shard.candidate_order``'s numb
 set bits are exactly the (key, SSTable) pairs the reference would go on to read, in the
 reference's order (``candidate_lists``).  A level SSTable whose range holds no key of the batch
 is never probed, as the reference never probes it.
+
+``candidates_one`` is the per-key form (one ``get``): the range checks are Python's own ``str``
+comparison on the host, and every L0 filter plus every in-range level filter is tested in ONE
+launch (``pbf_may_contain_set``), whatever the filters' sizes — instead of one ``may_contain``
+launch per SSTable.
 """
 from __future__ import annotations
 
@@ -25,7 +30,7 @@ from typing import NamedTuple, Sequence
 import numpy as np
 
 from . import _native
-from .bloom_filter import BloomFilter, _default_device, may_contain_multi
+from .bloom_filter import BloomFilter, _default_device, may_contain_multi, may_contain_set
 from .keys import PackedKeys
 
 
@@ -92,3 +97,19 @@ def candidate_lists(masks: np.ndarray, n: int) -> list[list[int]]:
     """Per key, the SSTable rows of ``candidate_masks`` in the reference's read order."""
     bits = np.unpackbits(masks, axis=1, bitorder="little")[:, :n].astype(bool)
     return [[int(t) for t in np.flatnonzero(bits[:, i])] for i in range(n)]
+
+
+def candidates_one(key: str, level0: Sequence[BloomFilter], levels: Sequence[Sequence[LevelTable]]) -> list[int]:
+    """The SSTables ``LsmStorage.get(key)`` would read if none held the key, in its order
+    (lsm_storage.py:164-179), numbered as ``candidate_masks`` rows: L0 filters (newest first)
+    and the level filters whose ``first_key <= key <= last_key`` (:173) are tested together in
+    one ``pbf_may_contain_set`` launch."""
+    flat = [t for lvl in levels for t in lvl]
+    in_range = [j for j, t in enumerate(flat) if t.first_key <= key <= t.last_key]
+    tested = list(level0) + [flat[j].bloom_filter for j in in_range]
+    if not tested:
+        return []
+    hits = may_contain_set(tested, key)
+    out = [t for t in range(len(level0)) if hits[t]]
+    out += [len(level0) + j for r, j in enumerate(in_range) if hits[len(level0) + r]]
+    return out

@@ -137,33 +137,81 @@ def test_config4_full_size_product_sizing(oracle):
 
 
 @pytest.mark.timeout(150)
+def test_config4_eight_concurrent_builds_and_absent_keys(oracle):
+    """C4 as bench.py runs it (BASELINE configs[3]): the eight 125M-key product-sized filters
+    (nb_bytes 224,649,806, k = 10) cleared and built back to back on their own pooled streams with
+    no wait between them, twice.  Filters 0 and 6 == the C oracle bit for bit; filter 6's hit
+    mask of 1M absent keys == the oracle's bitwise (the reference's non-uniform floor-mod for a
+    non-power-of-two m shows in its false-positive rate)."""
+    from math import ceil, log
+    n = 125_000_000
+    m = (-n * log(0.001)) / (log(2) ** 2)
+    nb, k = ceil(m / 8), round((m / n) * log(2))
+    keys = [dev_keys_hex(0x5EEDB100, g * n, n) for g in range(8)]
+    fs = [BloomFilter(nb, k) for _ in range(8)]
+    assert len({bf.stream for bf in fs}) > 1  # the pool deals distinct streams
+    for _ in range(2):
+        for g, bf in enumerate(fs):
+            bf.clear()
+            bf.add_device_fixed(keys[g].data_ptr(), 16, n)
+    absent = dev_keys_hex(0x5EEDB100, 8 * n, 1_000_000)
+    hm = torch.zeros(1_000_000 // 8, dtype=torch.uint8, device="cuda")
+    fs[6].probe_device_fixed(absent.data_ptr(), 16, 1_000_000, hm.data_ptr())
+    for bf in fs:
+        bf.sync()
+    assert all(bf.last_build_mode == PBF_BUILD_TILED for bf in fs)
+    got = {g: fs[g].bitmap() for g in (0, 6)}
+    host = {g: PackedKeys.fixed(keys[g].cpu().numpy().reshape(-1, 16)) for g in (0, 6)}
+    hm_got = hm.cpu().numpy()
+    del keys, absent, hm
+    for g in (0, 6):
+        want = oracle.build(nb, k, host[g], omp=True)
+        assert got[g] == want.tobytes(), g
+        if g == 6:
+            qs = PackedKeys.fixed(splitmix_hex_keys(0x5EEDB100, 8 * n, 1_000_000))
+            want_hm = oracle.probe(want, k, qs, omp=True)
+            assert np.array_equal(hm_got, want_hm)
+            fp = int(np.unpackbits(hm_got).sum())
+            assert 500 < fp < 2500, fp  # ~0.0013 (the floor-mod's edge tiles), not 0.001
+
+
+@pytest.mark.timeout(150)
 def test_config3_full_size_varlen_large_m(oracle):
-    """C3: 100M variable-length keys (8..64 B) into m = 2^33 bits (nb_bytes = 2^30), k = 8 — the
-    m > 2^32 index map where only [0, 2^31) and [m - 2^31, m) are reachable.  Tiled build ==
-    the C oracle bit for bit; members all hit; the unreachable middle stays zero."""
+    """C3 as bench.py runs it (BASELINE configs[2]): 100M variable-length keys (8..64 B) into
+    m = 2^33 bits (nb_bytes = 2^30), k = 8 — the m > 2^32 index map where only [0, 2^31) and
+    [m - 2^31, m) are reachable — then ONE probe of 200M keys (the 100M members + 100M absent:
+    two tiled pipelines, the counting-sort partition at 4096 tiles).  Build == the C oracle bit
+    for bit, the unreachable middle stays zero, members all hit, and the absent half's hit mask
+    == the oracle's bitwise (every false positive the same)."""
     from pebbledb_amd.keys import _splitmix64_np
     n, nb, k = 100_000_000, 2 ** 30, 8
-    idx = np.arange(n, dtype=np.uint64)
+    idx = np.arange(2 * n, dtype=np.uint64)
     with np.errstate(over="ignore"):
         h = _splitmix64_np((np.uint64(0xC3) << np.uint64(32)) + idx)
-    o = np.zeros(n + 1, dtype=np.uint64)
+    o = np.zeros(2 * n + 1, dtype=np.uint64)
     np.cumsum((np.uint64(8) + h % np.uint64(57)), out=o[1:])
     del h, idx
     od = torch.from_numpy(o.view(np.int64)).cuda()
     d = torch.empty(int(o[-1]), dtype=torch.uint8, device="cuda")
     torch.cuda.synchronize()
-    _native.check(_native.lib().pbf_gen_varlen(0, None, d.data_ptr(), od.data_ptr(), 0xC3, 0, n), "gen")
+    _native.check(_native.lib().pbf_gen_varlen(0, None, d.data_ptr(), od.data_ptr(), 0xC3, 0, 2 * n), "gen")
     torch.cuda.synchronize()
     bf = BloomFilter(nb, k)
     bf.set_build_mode(PBF_BUILD_TILED)
     bf.add_device(d.data_ptr(), od.data_ptr(), n)
-    hm = torch.zeros(n // 8, dtype=torch.uint8, device="cuda")
-    bf.probe_device(d.data_ptr(), od.data_ptr(), n, hm.data_ptr())
+    hm = torch.zeros(2 * n // 8, dtype=torch.uint8, device="cuda")
+    bf.probe_device(d.data_ptr(), od.data_ptr(), 2 * n, hm.data_ptr())
     bf.sync()
-    assert bool((hm == 0xFF).all().item())
+    assert bf.last_probe_mode == PBF_PROBE_TILED
+    h_all = hm.cpu().numpy()
+    assert (h_all[: n // 8] == 0xFF).all()
     got = np.frombuffer(bf.bitmap(), dtype=np.uint8)
     assert not got[2 ** 28: nb - 2 ** 28].any()  # bits [2^31, m - 2^31) are unreachable
-    host = PackedKeys(d.cpu().numpy(), n, offsets=o)
+    hd = d.cpu().numpy()
     del d, od, hm
-    want = oracle.build(nb, k, host, omp=True)
+    want = oracle.build(nb, k, PackedKeys(hd[: int(o[n])], n, offsets=o[: n + 1]), omp=True)
     assert np.array_equal(got, want)
+    absent = PackedKeys(hd[int(o[n]):], n, offsets=o[n:] - o[n])
+    want_hm = oracle.probe(want, k, absent, omp=True)
+    assert np.array_equal(h_all[n // 8:], want_hm)
+    assert 30 < int(np.unpackbits(want_hm).sum()) < 300  # ~116 at these seeds (~70 expected)

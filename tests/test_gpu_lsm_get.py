@@ -10,7 +10,8 @@ import pytest
 
 from pebbledb_amd import BloomFilter, PackedKeys
 from pebbledb_amd import _native
-from pebbledb_amd.lsm_get import LevelTable, candidate_lists, candidate_masks, key_range_masks
+from pebbledb_amd.lsm_get import LevelTable, candidate_lists, candidate_masks, candidates_one, key_range_masks
+from conftest import load_golden
 
 pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
@@ -114,3 +115,44 @@ def test_candidate_order_equals_reference_get_loop(oracle):
     assert got == want
     assert not masks[len(l0) + 7].any()  # the unreached L2 table
     assert any(len(c) > 3 for c in got)  # the fixture exercises several levels per key
+
+
+def _golden_store():
+    """The store of tests/golden/lsm_get_order.json (tools/gen_golden_lsm.py: the REAL
+    reference's LsmStorage.get, src/lsm_storage.py:153-181, with every SSTable.get recorded):
+    each table's filter built here with the product sizing (sstable.py:274) and checked against
+    the reference's own bitmap."""
+    import hashlib
+    g = load_golden("lsm_get_order.json")
+    U = g["universe"]
+    l0, levels = [], [[], []]
+    for t in g["tables"]:
+        keys = U[t["start"]:t["stop"]:t["step"]]
+        bf = BloomFilter.build_from_keys_and_fp_rate(keys, g["fp_rate"])
+        assert (bf.nb_bytes, bf.nb_hash_functions) == (t["nb_bytes"], t["k"])
+        bm = bf.bitmap()
+        assert hashlib.sha256(bm).hexdigest() == t["sha256"] and sum(bin(b).count("1") for b in bm) == t["popcount"]
+        assert (keys[0], keys[-1]) == (t["first_key"], t["last_key"])
+        if t["level"] == 0:
+            l0.append(bf)
+        else:
+            levels[t["level"] - 1].append(LevelTable(t["first_key"], t["last_key"], bf))
+    return g, l0, levels
+
+
+def test_candidate_order_equals_reference_lsm_get_golden():
+    """Batched filter stage (candidate_masks: mixed-size L0 filters through the fused multi-filter
+    probe, level ranges on the device) == the SSTable reads the real reference's get made."""
+    g, l0, levels = _golden_store()
+    masks = candidate_masks(g["probes"], l0, levels)
+    assert candidate_lists(masks, len(g["probes"])) == g["order"]
+    assert l0[0].last_probe_detail & _native.PBF_DETAIL_SET  # mixed sizes: one fused launch
+
+
+def test_per_key_get_one_launch_equals_reference_lsm_get_golden():
+    """The per-key form (candidates_one: host range check + ONE pbf_may_contain_set launch over
+    the L0 and in-range level filters, all of different sizes) == the reference's get, key by key."""
+    g, l0, levels = _golden_store()
+    for key, want in zip(g["probes"], g["order"]):
+        assert candidates_one(key, l0, levels) == want, key
+    assert l0[0].last_probe_detail == _native.PBF_DETAIL_ONE_KEY | _native.PBF_DETAIL_SET

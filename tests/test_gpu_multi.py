@@ -4,7 +4,7 @@ config C5).  Every hit mask must equal the filter's own single probe and the ora
 import numpy as np
 import pytest
 
-from pebbledb_amd import BloomFilter, PackedKeys, may_contain_multi, probe_multi_device
+from pebbledb_amd import BloomFilter, PackedKeys, may_contain_multi, may_contain_set, probe_multi_device
 from pebbledb_amd import _native
 from pebbledb_amd._native import PBF_PROBE_DIRECT, PBF_PROBE_TILED
 from pebbledb_amd.keys import splitmix_hex_keys, varlen_keys
@@ -74,6 +74,82 @@ def test_multi_mixed_sizes_k0_and_varlen(oracle):
     fs[2].set_probe_mode(PBF_PROBE_TILED)
     got2 = may_contain_multi([fs[0], fs[2]], q)
     assert np.array_equal(got2[0], got[0]) and np.array_equal(got2[1], got[2])
+
+
+def _product_filters(oracle, ns, seed=SEED):
+    """SSTable filters as pebbledb sizes them (sstable.py:274: fp 0.001 -> k = 10, nb_bytes from
+    each table's own key count): every filter a different nb_bytes."""
+    fs, want, start = [], [], 0
+    for n in ns:
+        pk = PackedKeys.fixed(splitmix_hex_keys(seed, start, n))
+        bf = BloomFilter.build_from_keys_and_fp_rate(pk, 0.001)
+        fs.append(bf)
+        want.append(oracle.build(bf.nb_bytes, bf.nb_hash_functions, pk))
+        start += n
+    return fs, want, start
+
+
+def test_multi_mixed_product_sizes_one_hash_pass(oracle):
+    """8 product-sized filters of different n (different nb_bytes, k = 10): one k_probe_set launch
+    hashes every key once for all eight; each hit mask equals the filter's own probe and the
+    oracle, host- and device-resident.  Then a set mixing them with a large filter (its own tiled
+    pipeline) and a k = 7 filter (its own fused group)."""
+    ns = [150_000 * (i + 1) for i in range(8)]  # 150k .. 1.2M keys: 270 KB .. 2.2 MB filters
+    fs, want, total = _product_filters(oracle, ns)
+    assert len({bf.nb_bytes for bf in fs}) == 8 and {bf.nb_hash_functions for bf in fs} == {10}
+    q = PackedKeys.fixed(splitmix_hex_keys(SEED, total // 2, total + 37))  # members of the later filters + absent
+    got = may_contain_multi(fs, q)
+    assert all(bf.last_probe_detail == (_native.PBF_DETAIL_SET | (8 << 8)) for bf in fs)
+    for i, bf in enumerate(fs):
+        assert np.array_equal(got[i], oracle.probe(want[i], 10, q)), i
+        assert np.array_equal(got[i], bf.may_contain_many(q, packed=True)), i
+    assert got[-1].any() and not got[-1].all()
+    # device-resident keys and hit masks
+    qd = torch.from_numpy(q.data.copy()).cuda()
+    hm = torch.zeros((len(fs), (q.n + 7) // 8), dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    probe_multi_device(fs, qd.data_ptr(), q.n, [hm[i].data_ptr() for i in range(len(fs))], key_len=16)
+    fs[0].sync()
+    assert np.array_equal(hm.cpu().numpy(), got)
+    # mixed with a large filter (tiled: its own pipeline and stream) and a k = 7 one
+    big_pk = PackedKeys.fixed(splitmix_hex_keys(SEED + 1, 0, 3_000_000))
+    big = BloomFilter(2 ** 25, 6)
+    big.add_many(big_pk)
+    seven = BloomFilter(300_007, 7)
+    seven.add_many(PackedKeys.fixed(splitmix_hex_keys(SEED + 2, 0, 200_000)))
+    want7 = oracle.build(300_007, 7, PackedKeys.fixed(splitmix_hex_keys(SEED + 2, 0, 200_000)))
+    wantb = oracle.build(2 ** 25, 6, big_pk)
+    mixed = [fs[3], big, seven, fs[0], fs[7]]
+    got2 = may_contain_multi(mixed, q)
+    assert big.last_probe_mode == PBF_PROBE_TILED
+    assert np.array_equal(got2[0], got[3]) and np.array_equal(got2[3], got[0]) and np.array_equal(got2[4], got[7])
+    assert np.array_equal(got2[1], oracle.probe(wantb, 6, q))
+    assert np.array_equal(got2[2], oracle.probe(want7, 7, q))
+
+
+def test_may_contain_set_one_key_many_sizes(oracle):
+    """pbf_may_contain_set: one key against 16 L0-like and 6 level-like filters of different sizes
+    (product sizing), a k = 7 and a k = 0 filter and a repeated filter, in one launch per k;
+    every answer equals the filter's own may_contain and the oracle's.  Keys: members, absent
+    keys, empty, non-ASCII, and a key longer than the 4 KiB mapped stage."""
+    ns = [20_000 + 7_919 * i for i in range(22)]
+    fs, want, total = _product_filters(oracle, ns, seed=SEED + 5)
+    seven = BloomFilter(50_021, 7)
+    seven.add_many(["k%d" % i for i in range(3000)])
+    zero = BloomFilter(64, 0)
+    mixed = fs[:10] + [seven, zero] + fs[10:] + [fs[4]]
+    keys = [bytes(k).decode() for k in splitmix_hex_keys(SEED + 5, 0, total)[::997]]
+    keys += [bytes(k).decode() for k in splitmix_hex_keys(SEED + 6, 0, 120)] + ["", "é\U0001f511", "x" * 5000]
+    keys += ["k%d" % i for i in range(0, 4000, 37)]
+    for key in keys:
+        got = may_contain_set(mixed, key)
+        assert got == [bf.may_contain(key) for bf in mixed], key
+    w7 = oracle.build(50_021, 7, PackedKeys.from_strs(["k%d" % i for i in range(3000)]))
+    pk = PackedKeys.from_strs(keys)
+    for bf, w in zip(fs + [seven], want + [w7]):
+        hits = np.unpackbits(oracle.probe(w, bf.nb_hash_functions, pk), bitorder="little")[:len(keys)]
+        assert [bool(h) for h in hits] == [may_contain_set([bf], key)[0] for key in keys]
+    assert may_contain_set([], "a") == []
 
 
 def test_multi_rejects_bad_sets():

@@ -156,3 +156,23 @@ def test_omp_twins_equal_serial(oracle):
     assert (a == b).all()
     q = PackedKeys.fixed(splitmix_hex_keys(7, 25000, 50001))
     assert (oracle.probe(a, 6, q) == oracle.probe(a, 6, q, omp=True)).all()
+
+
+def test_lsm_get_restatement_equals_reference_golden(oracle):
+    """oracle/lsm_get_oracle.py (the restated filter stage of LsmStorage.get) against the SSTable
+    reads the REAL reference's get made (tests/golden/lsm_get_order.json, tools/gen_golden_lsm.py):
+    13 product-sized filters of 9 different sizes over L0 and two levels, 1357 probe keys."""
+    from oracle.lsm_get_oracle import reference_candidates
+    g = load_golden("lsm_get_order.json")
+    U = g["universe"]
+    l0, levels = [], [[], []]
+    for t in g["tables"]:
+        keys = U[t["start"]:t["stop"]:t["step"]]
+        assert sizing(len(keys), g["fp_rate"]) == (t["nb_bytes"], t["k"])
+        bm = oracle.build(t["nb_bytes"], t["k"], PackedKeys.from_strs(keys))
+        assert hashlib.sha256(bm.tobytes()).hexdigest() == t["sha256"]
+        if t["level"] == 0:
+            l0.append((bm, t["k"]))
+        else:
+            levels[t["level"] - 1].append((t["first_key"], t["last_key"], bm, t["k"]))
+    assert reference_candidates(g["probes"], l0, levels) == g["order"]
