@@ -48,7 +48,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS) + ["c4", "c5", "sst"])
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS) + ["c4", "c5", "c5mixed", "sst"])
     ap.add_argument("--c4-keys", type=int, default=125_000_000, help="c4: keys per filter (reference 125M)")
     ap.add_argument("--c5-probes", type=int, default=100_000_000, help="c5: probe keys (reference 100M)")
     ap.add_argument("--build-mode", type=int, default=0, help="0 auto, 1 atomic, 2 tiled")
@@ -223,7 +223,39 @@ def dropin_latency(device, reps=2000):
             out[name]["build_from_keys_1k_us"] = round(t_bk / 20 * 1e6, 1)
     out["identical"] = (out["pebbledb_amd"]["bitmap_sha16"] == out["reference_port"]["bitmap_sha16"]
                         and out["pebbledb_amd"]["hits"] == out["reference_port"]["hits"])
+    out["get_16_filters"] = get_set_latency(device)
     return out
+
+
+def get_set_latency(device, reps=1000):
+    """One LsmStorage.get's bloom checks (src/lsm_storage.py:164-179) over 10 L0 + 6 level SSTable
+    filters of 16 different sizes (product sizing, sstable.py:274: 20k..170k keys, k = 10): one
+    pbf_may_contain_set launch (lsm_get.candidates_one) vs 16 may_contain calls (one launch each);
+    the answers must be identical."""
+    from pebbledb_amd import BloomFilter
+    from pebbledb_amd.keys import splitmix_hex_keys_str
+    from pebbledb_amd.lsm_get import LevelTable, candidates_one
+    ns = [20_000 + 10_000 * i for i in range(16)]
+    tables, start = [], 0
+    for n in ns:
+        keys = sorted(splitmix_hex_keys_str(SEED, start, n))
+        tables.append((keys[0], keys[-1], BloomFilter.build_from_keys_and_fp_rate(keys, 0.001, device=device)))
+        start += n
+    l0 = [bf for _, _, bf in tables[:10]]
+    levels = [[LevelTable("", "\U0010ffff", bf) for _, _, bf in tables[10:]]]  # ranges that hold every probe
+    flat = l0 + [t.bloom_filter for t in levels[0]]
+    probes = splitmix_hex_keys_str(SEED, start - 500, 1000)  # 500 members of the last table, 500 absent
+    for key in probes[:50]:
+        candidates_one(key, l0, levels)
+    t0 = time.perf_counter()
+    one = [candidates_one(probes[i % 1000], l0, levels) for i in range(reps)]
+    t_set = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    loop = [[t for t, bf in enumerate(flat) if bf.may_contain(probes[i % 1000])] for i in range(reps)]
+    t_loop = time.perf_counter() - t0
+    return {"filters": len(flat), "nb_bytes": [bf.nb_bytes for bf in flat],
+            "one_launch_us_per_get": round(t_set / reps * 1e6, 2),
+            "may_contain_x16_us_per_get": round(t_loop / reps * 1e6, 2), "identical": one == loop}
 
 
 def all_reduce_scalar(torch, dist, value, op, dtype):
@@ -487,6 +519,132 @@ def sets_main(args, rank, world, local, torch, dist, np):
         print(json.dumps(out), flush=True)
 
 
+def mixed_main(args, rank, world, local, torch, dist, np):
+    """c5mixed — the batched LsmStorage.get filter stage (src/lsm_storage.py:164-179) over SSTable
+    filters of DIFFERENT sizes, as an LSM has them (each sized from its own key count,
+    sstable.py:274: fp 0.001 -> k = 10): 8 filters of 0.5M..4M keys (nb_bytes 0.9..7.2 MB) and
+    a batch of 36M 16-B keys (the 18M members + 18M absent) in HBM.  A step = one
+    pbf_probe_multi of the batch against the rank's filters: one k_probe_set launch that hashes
+    every key once and tests every filter.  Beside it the previous behaviour, one probe pipeline
+    per filter (each re-reading and re-hashing the batch).  value = key x filter probes / s."""
+    from math import ceil, log
+
+    from oracle.oracle import COracle
+    from pebbledb_amd import BloomFilter, PackedKeys, _native, probe_multi_device
+    from pebbledb_amd.bloom_filter import set_default_device
+    from pebbledb_amd.keys import splitmix_hex_keys
+    from pebbledb_amd.shard import filters_for_rank
+
+    set_default_device(local)
+    L = _native.lib()
+    mine = filters_for_rank(8, world, rank)
+    ns = [500_000 * (g + 1) for g in range(8)]
+    starts = [sum(ns[:g]) for g in range(8)]
+    total = sum(ns)
+    nq = 2 * total
+    q = torch.empty(nq * 16, dtype=torch.uint8, device="cuda")
+    _native.check(L.pbf_gen_splitmix_hex(local, None, q.data_ptr(), SEED, 0, nq), "gen")
+    torch.cuda.synchronize()
+    filters = {}
+    for g in mine:
+        m = (-ns[g] * log(0.001)) / (log(2) ** 2)  # bloom_filter.py:109-114, same expression order
+        bf = BloomFilter(ceil(m / 8), round((m / ns[g]) * log(2)), device=local)
+        bf.add_device_fixed(q.data_ptr() + starts[g] * 16, 16, ns[g])
+        bf.sync()
+        filters[g] = bf
+    fl = [filters[g] for g in mine]
+    k = fl[0].nb_hash_functions
+    hms = {g: torch.zeros((nq + 7) // 8, dtype=torch.uint8, device="cuda") for g in mine}
+    stream = torch.cuda.ExternalStream(fl[0].stream)
+
+    def fused():
+        probe_multi_device(fl, q.data_ptr(), nq, [hms[g].data_ptr() for g in mine], key_len=16)
+
+    def per_filter():
+        for g in mine:
+            filters[g].probe_device_fixed(q.data_ptr(), 16, nq, hms[g].data_ptr())
+
+    def timed(fn):
+        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(args.steps)]
+        for _ in range(args.warmup):
+            fn()
+        for bf in fl:
+            bf.sync()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for st in range(args.steps):
+            evs[st][0].record(stream)
+            fn()
+            evs[st][1].record(stream)
+        for bf in fl:
+            bf.sync()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        if world > 1:
+            el = float(all_reduce_scalar(torch, dist, el, dist.ReduceOp.MAX, torch.float64))
+        return el / args.steps * 1e3, sum(a.elapsed_time(b) for a, b in evs) / args.steps
+
+    ms_pf, _ = timed(per_filter)
+    got_pf = {g: hms[g].cpu().numpy().copy() for g in mine}
+    ms, pass_ms = timed(fused)
+    got = {g: hms[g].cpu().numpy() for g in mine}
+    ok = all(np.array_equal(got[g], got_pf[g]) for g in mine)
+    fp_total, fp_expect = 0, 0.0
+    for g in mine:
+        bits = np.unpackbits(got[g], bitorder="little")[:nq]
+        ok &= bool(bits[starts[g]:starts[g] + ns[g]].all())
+        fill = filters[g].popcount() / (8 * filters[g].nb_bytes)
+        fp_total += int(bits[total:].sum())
+        fp_expect += total * fill ** k
+    fp_ok = fp_total <= 3 * fp_expect + 20 * len(mine)
+    if world > 1:
+        ok = bool(all_reduce_scalar(torch, dist, 1 if ok else 0, dist.ReduceOp.MIN, torch.int32))
+    if rank != 0:
+        return
+    # SURVEY.md §8d probe bytes with the key read once for the set: nq*L + nf*(4*nq*k + nq/8)
+    b_pass = nq * 16 + len(mine) * (4 * nq * k + nq // 8)
+    ach = b_pass / (pass_ms * 1e-3) / 1e9
+    out = {
+        "metric": "Mprobes/s (key x filter) batched probe, 36M keys vs 8 mixed-size product-sized filters",
+        "value": round(nq * 8 / (ms * 1e-3) / 1e6, 3), "unit": "Mprobes/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "u32",
+        "data": "synthetic (splitmix64 hex keys generated on device)",
+        "config": {"workload": (f"c5mixed: {nq} probe keys (half members) x 8 product-sized filters of "
+                                f"{ns[0]}..{ns[-1]} keys (fp 0.001, k={k}); filters {len(mine)}/rank"),
+                   "nb_bytes": [filters[g].nb_bytes for g in mine], "k": k,
+                   "parallelism": f"filters-over-gpus x{world}"},
+        "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                     "kernel": "k_probe_set (each key hashed once, every filter tested; bitmaps Infinity-Cache resident)",
+                     "algorithmic_bytes": int(b_pass), "avg_ms": round(pass_ms, 4)},
+        "per_filter_pipelines_ms": round(ms_pf, 4), "speedup_vs_per_filter": round(ms_pf / ms, 2),
+        "check": {"members_all_hit": ok, "equal_to_per_filter_probes": ok, "false_positives": fp_total,
+                  "fp_expected": round(fp_expect, 1), "fp_within_3x_expected": bool(fp_ok),
+                  "probe_detail": hex(fl[0].last_probe_detail)},
+        **dist_report(dist, world),
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        # the C oracle (OpenMP, all host cores) on a 2M-key sample against every filter, and the
+        # sample's hit masks equal to the device's
+        o = COracle()
+        ns_s = 2_000_000
+        sample = PackedKeys.fixed(splitmix_hex_keys(SEED, total - ns_s // 2, ns_s))
+        bms = [np.frombuffer(filters[g].bitmap(), dtype=np.uint8).copy() for g in mine]
+        t0 = time.perf_counter()
+        hs = [o.probe(bm, k, sample, omp=True) for bm in bms]
+        t_cpu = time.perf_counter() - t0
+        off = (total - ns_s // 2) // 8
+        same = all(np.array_equal(h, got[g][off:off + ns_s // 8]) for h, g in zip(hs, mine))
+        out["cpu_baseline"] = {"value": round(ns_s * len(mine) / t_cpu / 1e6, 3), "unit": "Mprobes/s",
+                               "cores": o.num_threads(), "kind": "port",
+                               "sample": f"C oracle, {ns_s} keys x {len(mine)} filters (OpenMP)"}
+        out["check"]["oracle_sample_equal"] = same
+    print(json.dumps(out), flush=True)
+
+
 def sst_main(args, rank, world, local, torch, dist, np):
     """SSTable data-section encode (sstable.py:224-268): one flush-sized
     SSTable per GPU — 3.5M records of a 16-B hex key and a 48-B value (72 B encoded, 252 MB of
@@ -714,6 +872,11 @@ def main():
         else:
             dist.init_process_group(backend=backend, init_method="env://")
 
+    if args.config == "c5mixed":
+        mixed_main(args, rank, world, local, torch, dist, np)
+        if world > 1:
+            dist.destroy_process_group()
+        return
     if args.config == "sst":
         sst_main(args, rank, world, local, torch, dist, np)
         if world > 1:

@@ -1035,7 +1035,49 @@ bool set_direct(pbf_filter_t* f, uint64_t n) {
     return kmax_for(f->k) > 0 && (f->probe_mode == PBF_PROBE_DIRECT || !want_tiled_probe(f, n));
 }
 
-// One launch of k_probe_set per (k, up to 64 filters): every key is hashed once for the group.
+// The 8 XCD slots of one k_probe_set launch (set_kernels.hpp): with nf <= 8 filters, slot x
+// takes filter x % nf and 1/(slots of that filter) of the keys; with more, the filters are dealt
+// largest first onto the slot with the fewest bitmap bytes so far, each slot all the keys.
+XcdPlan plan_xcd(const std::vector<pbf_filter_t*>& grp, size_t g0, uint32_t nf) {
+    XcdPlan xp{};
+    if (nf <= 8) {
+        uint32_t at = 0;
+        for (uint32_t f = 0; f < nf; ++f) {
+            const uint32_t parts = 8 / nf + (f < 8 % nf ? 1u : 0u);
+            for (uint32_t p = 0; p < parts; ++p) {
+                const uint32_t x = f + p * nf;
+                xp.first[x] = uint8_t(at);
+                xp.count[x] = 1;
+                xp.part[x] = uint8_t(p);
+                xp.nparts[x] = uint8_t(parts);
+            }
+            xp.order[at++] = uint8_t(f);
+        }
+        return xp;
+    }
+    std::vector<uint32_t> idx(nf);
+    for (uint32_t f = 0; f < nf; ++f) idx[f] = f;
+    std::stable_sort(idx.begin(), idx.end(),
+                     [&](uint32_t a, uint32_t b) { return grp[g0 + a]->nb_bytes > grp[g0 + b]->nb_bytes; });
+    std::vector<std::vector<uint32_t>> slot(8);
+    uint64_t load[8] = {};
+    for (uint32_t f : idx) {
+        const int x = int(std::min_element(load, load + 8) - load);
+        slot[x].push_back(f);
+        load[x] += grp[g0 + f]->nb_bytes;
+    }
+    uint32_t at = 0;
+    for (int x = 0; x < 8; ++x) {
+        xp.first[x] = uint8_t(at);
+        xp.count[x] = uint8_t(slot[x].size());
+        xp.part[x] = 0;
+        xp.nparts[x] = 1;
+        for (uint32_t f : slot[x]) xp.order[at++] = uint8_t(f);
+    }
+    return xp;
+}
+
+// One launch of k_probe_set per (k, up to 64 filters).
 int probe_set_direct(pbf_filter_t* f0, std::vector<pbf_filter_t*>& grp, std::vector<uint8_t*>& hms, const Batch& b) {
     const uint32_t k = grp[0]->k;
     for (size_t g0 = 0; g0 < grp.size(); g0 += kMaxFilterSet) {
@@ -1046,11 +1088,13 @@ int probe_set_direct(pbf_filter_t* f0, std::vector<pbf_filter_t*>& grp, std::vec
             fset.im[i] = grp[g0 + i]->im;
             fset.hm[i] = hms[g0 + i];
         }
-        const uint32_t grid = grid_for(b.n, 256, 1u << 20);
+        const XcdPlan xp = plan_xcd(grp, g0, fset.nf);
+        // 8 slots x up to 512 workgroups of 256 keys
+        const uint32_t grid = 8 * grid_for((b.n + 7) / 8, 256, 512);
         dispatch(kmax_for(k), b.km, [&](auto KMAX, auto KM) {
             if constexpr (decltype(KMAX)::value > 0)
                 k_probe_set<decltype(KMAX)::value, decltype(KM)::value>
-                    <<<grid, 256, 0, f0->stream>>>(b.ks, b.n, int(k), fset);
+                    <<<grid, 256, 0, f0->stream>>>(b.ks, b.n, int(k), fset, xp);
         });
         LAUNCHED(f0, "k_probe_set");
     }

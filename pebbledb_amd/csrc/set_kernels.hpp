@@ -6,10 +6,11 @@
 // 256 MB holds a few million keys: its filter is a few MB.  MurmurHash3 does not depend on m —
 // only the floor-mod does — so a key is hashed ONCE (k seeds) and every filter of the set is
 // tested from those k hashes:
-//   * k_probe_set: one lane per key of a batch; the first two words of every filter of a pass
-//     are loaded together (2 x nf loads in flight per lane), the rest only for lanes that are
-//     still possible members of that filter (bloom_filter.py:71-73's early exit); one wave64
-//     ballot per filter writes that filter's LSB-first hit-mask word.
+//   * k_probe_set: one lane per key of a batch, the filters spread over the 8 XCDs (XcdPlan) so
+//     each XCD's L2 holds only its own filters; a key is hashed once per XCD slot for all of the
+//     slot's filters.  The first two words of every filter of a pass are loaded together, the
+//     rest only for lanes that are still possible members of that filter (bloom_filter.py:
+//     71-73's early exit); one wave64 ballot per filter writes its LSB-first hit-mask word.
 //   * k_may_contain_set: ONE key against up to 64 filters per launch (the per-key form of
 //     LsmStorage.get): every lane hashes the key (a wave's worth of redundant ALU instead of a
 //     hash broadcast), lane f tests filter f, one ballot is the answer; key in and answer out
@@ -37,26 +38,45 @@ __device__ __forceinline__ uint32_t test_bit(const uint32_t* __restrict__ bm, ui
     return (bm[idx >> 5] >> (idx & 31)) & 1u;
 }
 
-// fs.hm[f]: filter f's LSB-first hit mask of the n keys.
+// Filters per XCD: workgroups are dealt round-robin over the 8 XCDs in dispatch order (block i
+// and block i + 8 run on the same XCD; speed only, never correctness), so the workgroups of
+// slot x = blockIdx % 8 share one XCD and its 4 MiB L2.  Slot x tests the filters
+// order[first[x] .. first[x] + count[x]) over its part `part[x]` of `nparts[x]` of the batch.
+// With fewer than 8 filters a filter spans several slots (keys split between them); with more,
+// a slot holds several (each of its keys hashed once for all of them).
+struct XcdPlan {
+    uint8_t first[8], count[8], part[8], nparts[8];
+    uint8_t order[kMaxFilterSet];
+};
+
+// fs.hm[f]: filter f's LSB-first hit mask of the n keys.  The direct probe is bound by the rate
+// of random 4-B requests; a filter whose requests all come from one XCD stays in that XCD's L2
+// (C5mixed: all eight filters tested by every workgroup measured 16.8 ms, one launch per filter
+// 12.7 ms, per-XCD slots below).
 template <int KMAX, int KM>
-__global__ void __launch_bounds__(256) k_probe_set(KeySet ks, uint64_t n, int k, FilterSet fs) {
-    const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
-    const uint32_t nf = fs.nf;
-    for (uint64_t base = uint64_t(blockIdx.x) * blockDim.x; base < n; base += stride) {
+__global__ void __launch_bounds__(256) k_probe_set(KeySet ks, uint64_t n, int k, FilterSet fs, XcdPlan xp) {
+    const uint32_t x = blockIdx.x & 7, jb = blockIdx.x >> 3, nbx = gridDim.x >> 3;
+    const uint32_t nfx = xp.count[x];
+    if (nfx == 0) return;
+    // the slot's key range, in whole 64-key hit-mask words
+    const uint64_t words = (n + 63) >> 6;
+    const uint64_t lo = min(n, (words * xp.part[x] / xp.nparts[x]) << 6);
+    const uint64_t hi = min(n, (words * (xp.part[x] + 1u) / xp.nparts[x]) << 6);
+    for (uint64_t base = lo + uint64_t(jb) * blockDim.x; base < hi; base += uint64_t(nbx) * blockDim.x) {
         const uint64_t i = base + threadIdx.x;
-        const bool live = i < n;
+        const bool live = i < hi;
         uint32_t h[KMAX];
 #pragma unroll
         for (int s = 0; s < KMAX; ++s) h[s] = 0;
         if (live) hash_key<KMAX, KM>(ks, i, k, [&](int s, uint32_t hv) { h[s] = hv; });
         const uint64_t key0 = base + (threadIdx.x & ~63u);
-        for (uint32_t f0 = 0; f0 < nf; f0 += kSetPass) {
+        for (uint32_t f0 = 0; f0 < nfx; f0 += kSetPass) {
             // stage 1: seeds 0 and 1 of every filter of the pass, all loads issued together
             uint32_t w[kSetPass][2];
 #pragma unroll
             for (int q = 0; q < kSetPass; ++q) {
-                const uint32_t f = f0 + q;
-                if (f < nf) {
+                if (f0 + q < nfx) {
+                    const uint32_t f = xp.order[xp.first[x] + f0 + q];
                     const IndexMap& im = fs.im[f];
 #pragma unroll
                     for (int s = 0; s < 2; ++s)
@@ -65,8 +85,8 @@ __global__ void __launch_bounds__(256) k_probe_set(KeySet ks, uint64_t n, int k,
             }
 #pragma unroll
             for (int q = 0; q < kSetPass; ++q) {
-                const uint32_t f = f0 + q;
-                if (f >= nf) break;
+                if (f0 + q >= nfx) break;
+                const uint32_t f = xp.order[xp.first[x] + f0 + q];
                 bool hit = live && (w[q][0] & w[q][1]);
                 if (hit) {  // the rest only for lanes still possibly members of filter f
                     const IndexMap& im = fs.im[f];
@@ -75,7 +95,7 @@ __global__ void __launch_bounds__(256) k_probe_set(KeySet ks, uint64_t n, int k,
                         if (s < k) hit &= test_bit(fs.bm[f], py_index(h[s], im)) != 0u;
                 }
                 const unsigned long long bal = __ballot(hit);
-                if ((threadIdx.x & 63) == 0 && key0 < n) store_hit_word(fs.hm[f], n, key0, bal);
+                if ((threadIdx.x & 63) == 0 && key0 < hi) store_hit_word(fs.hm[f], n, key0, bal);
             }
         }
     }
