@@ -357,8 +357,8 @@ __global__ void __launch_bounds__(512) k_gather_ring(TileMap tm, PartGeom pg, ui
             if constexpr (NFM == 1) {
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
-                    const uint32_t b = min(b0 + u * nwaves, b_hi - 1);
                     const uint32_t r = min(r0 + lane * 4, (max(fillb[u], 1u) - 1) & ~3u);
+                    const uint32_t b = min(b0 + u * nwaves, b_hi - 1);
                     rw[0][u] = rword(0, b, r);
                 }
 #pragma unroll
@@ -445,7 +445,8 @@ __global__ void __launch_bounds__(512) k_gather_ring(TileMap tm, PartGeom pg, ui
     lds_barrier();
     if (S > 1 || nf > 1) {
         for (uint32_t f = 0; f < nf; ++f)
-            for (uint32_t w = tid; w * 32 < nkeys; w += nt) atomicAnd(hw + f * neg_stride + (k0 >> 5) + w, kbits[f * kw + w]);
+            for (uint32_t w = tid; w * 32 < nkeys; w += nt)
+                atomicAnd(hw + f * neg_stride + (k0 >> 5) + w, kbits[f * kw + w]);
         return;
     }
     for (uint32_t w = tid; w * 32 < nkeys; w += nt) {

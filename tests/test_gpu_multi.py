@@ -226,7 +226,16 @@ def _c5_filters(oracle, nf, n_per, nb=2 ** 27, k=6):
     del keys
     want = [oracle.build(nb, k, PackedKeys.fixed(host[f * n_per:(f + 1) * n_per]), omp=True) for f in range(nf)]
     for f, bf in enumerate(fs):
-        assert bf.bitmap() == want[f].tobytes(), f
+        got = bf.bitmap()
+        if got != want[f].tobytes():
+            g = np.frombuffer(got, dtype=np.uint8)
+            missing = int(np.unpackbits(want[f] & ~g).sum())
+            extra = int(np.unpackbits(g & ~want[f]).sum())
+            tiles = np.unique(np.flatnonzero(g != want[f]) // (1 << 17))  # 2^20-bit tiles
+            raise AssertionError(f"filter {f}/{nf}: {missing} bits missing, {extra} extra, in tiles "
+                                 f"{tiles[:20].tolist()} ({len(tiles)} tiles); build detail "
+                                 f"{hex(bf.last_build_detail)} stream {bf.stream:#x}, streams "
+                                 f"{[hex(b.stream) for b in fs]}")
     return fs, want
 
 
