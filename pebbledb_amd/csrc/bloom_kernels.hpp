@@ -58,7 +58,7 @@ __device__ __forceinline__ void hash_key(const KeySet& ks, uint64_t i, int k, Em
         if constexpr (KMAX == 0) {
             murmur_seeds_loop(p, len, k, emit, sbase);
         } else {
-            murmur_seeds_chunked<KMAX>(p, len, k, emit, sbase);
+            murmur_seeds_seg<KMAX>(p, len, k, emit, sbase);
         }
     }
 }

@@ -111,7 +111,7 @@ __global__ void __launch_bounds__(64) k_may_contain_set(const uint8_t* __restric
     uint32_t h[KMAX];
 #pragma unroll
     for (int s = 0; s < KMAX; ++s) h[s] = 0;
-    murmur_seeds_chunked<KMAX>(key, len, k, [&](int s, uint32_t hv) { h[s] = hv; });
+    murmur_seeds_seg<KMAX>(key, len, k, [&](int s, uint32_t hv) { h[s] = hv; });
     bool hit = false;
     if (f < fs.nf) {
         const uint32_t* bm = fs.bm[f];

@@ -29,7 +29,7 @@ traffic() {  # tag bench-args...: FETCH_SIZE and WRITE_SIZE in separate passes, 
   local tag=$1; shift
   run pmc_fetch_$tag 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_fetch_$tag -o run -- python bench.py --no-cpu-baseline --no-host-inclusive "$@"
   run pmc_write_$tag 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_write_$tag -o run -- python bench.py --no-cpu-baseline --no-host-inclusive "$@"
-  python tools/traffic_summary.py gpurun_out/pmc_fetch_$tag gpurun_out/pmc_write_$tag gpurun_out/traffic_$tag.json > gpurun_out/traffic_${tag}_summary.txt 2>&1 || true
+  python tools/traffic_summary.py gpurun_out/pmc_fetch_$tag gpurun_out/pmc_write_$tag gpurun_out/traffic_$tag.json --config $tag > gpurun_out/traffic_${tag}_summary.txt 2>&1 || true
 }
 ab() {  # tag seconds rounds bench-args...
   local tag=$1 secs=$2 rounds=$3; shift 3
