@@ -225,7 +225,7 @@ namespace {
 // one for the duration of its host-side enqueue, and the GPU-side reuse across streams is
 // ordered by the set's `last` event (the next user's stream waits on it).
 struct Scratch {
-    DevBuf regions, fill, ovf, ovf_count, subcnt, rbits, neg, hw;
+    DevBuf regions, fill, ovf, ovf_count, pref, rbits, neg, hw;
     uint32_t ovf_phase = 0;  // which of the two overflow counters the next build uses
     bool ovf_init = false;
     DevBuf dkeys, doffs, dout;
@@ -236,7 +236,7 @@ struct Scratch {
     hipStream_t last_stream = nullptr;  // ... on this stream
     bool leased = false;
     void release_all() {
-        for (DevBuf* d : {&regions, &fill, &ovf, &ovf_count, &subcnt, &rbits, &neg, &hw, &dkeys, &doffs, &dout,
+        for (DevBuf* d : {&regions, &fill, &ovf, &ovf_count, &pref, &rbits, &neg, &hw, &dkeys, &doffs, &dout,
                           &svals, &splan, &ssec, &serr})
             d->release();
         pin[0].release();
@@ -620,7 +620,7 @@ void set_gather(PartPlan& pl, uint32_t B, uint32_t row, uint32_t nf = 1) {
     // the ring gather's quad table, when groups fit a byte and the workgroup stays small enough
     // for 4 per CU (measured neutral against the binary search, kept for the shorter path:
     // profiles/r02/s3/gsweep_*)
-    if (pl.pg.ring && row <= 255) {
+    if (row <= 255) {
         const uint32_t tq = pl.pg.cap / 4;
         const size_t with = ((pl.lds_gather + 3) & ~size_t(3)) + size_t((B + S - 1) / S) * tq + 4;
         if (with <= 38 * 1024) {
@@ -656,14 +656,15 @@ int part_kmax(uint32_t k, int km) {
     return kmax_for(k);
 }
 
-PartPlan plan_partition(uint32_t B, uint32_t k, int km, uint64_t n, bool probe, double share) {
+PartPlan plan_partition(uint32_t B, uint32_t k, int km, uint64_t n, bool probe, double share, uint32_t nf) {
     PartPlan pl{};
     const size_t per_entry = probe ? 6 : 4;  // stage u32 (+ u16 tile id for probes)
     const size_t fixed = size_t(3 * B + 1 + 16) * 4;
     // keys per thread per sub-chunk: as many as the registers (part_kpt) and the LDS allow
     uint64_t kpt = uint64_t(part_kpt(part_kmax(k, km), km, probe));
     while (kpt > 1 && fixed + kpt * kPartThreads * k * per_entry > 156 * 1024) --kpt;
-    if (probe) kpt = std::min<uint64_t>(kpt, (kSlotMask + 1) / kPartThreads);
+    // probe sub-chunks tile the 4096-key groups of the entry format: 1, 2 or 4 keys per thread
+    if (probe) kpt = kpt >= 4 ? 4 : (kpt >= 2 ? 2 : 1);
     const uint64_t kps = kpt * kPartThreads;
     pl.lds_part = fixed + size_t(kps) * k * per_entry;
     const uint64_t G0 = std::min<uint64_t>(part_max_groups(probe), std::max<uint64_t>(1, (n + kps - 1) / kps));
@@ -673,10 +674,11 @@ PartPlan plan_partition(uint32_t B, uint32_t k, int km, uint64_t n, bool probe, 
     pl.pg.kps = uint32_t(kps);
     pl.pg.kpw = kpw;
     pl.pg.nsub = uint32_t(kpw / kps);
+    pl.pg.nq = uint32_t((kpw + kGroupKeys - 1) / kGroupKeys);
     const double mu = double(kpw) * k * share;
     const uint64_t cap = uint64_t(mu + 8.0 * std::sqrt(mu) + 32.0);
     pl.pg.cap = uint32_t(((cap + 31) / 32) * 32);
-    set_gather(pl, B, pl.pg.nsub + 1);
+    set_gather(pl, B, pl.pg.nq + 1, nf);
     return pl;
 }
 
@@ -711,7 +713,7 @@ PartPlan plan_for(const TileMap& tm, uint32_t k, int km, uint64_t n, bool probe,
         // workgroup's regions are 32-bit (B * cap < 2^32)
         if (pl.pg.cap <= 32768 && uint64_t(B) * pl.pg.cap < (uint64_t(1) << 32)) return pl;
     }
-    return plan_partition(B, k, km, n, probe, share);
+    return plan_partition(B, k, km, n, probe, share, probe ? nf : 1);
 }
 
 // The ring partition kernel for (k, key layout): with the seed count fixed at compile time
@@ -789,7 +791,7 @@ int run_tiled(pbf_filter_t* f, const Batch& b) {
                     err = allow_lds(kern, pl.lds_part);
                     if (err == hipSuccess)
                         kern<<<pg.G, kPartThreads, pl.lds_part, s>>>(b.ks, b.n, int(k), tm, pg, regions, fill, nullptr,
-                                                             ovf, ovf_count, ProbeSet{});
+                                                             ovf, ovf_count, ProbeSet{}, nullptr);
                 });
             }
         }
@@ -819,29 +821,28 @@ int run_tiled_probe_set(pbf_filter_t* f, pbf_filter_t* const* fs, uint32_t nf, c
     const uint32_t k = f->k;
     const PartPlan pl = plan_for(tm, k, b.km, b.n, true, nf);
     const PartGeom& pg = pl.pg;
-    const uint32_t nfg = pg.ring ? nf : 1;  // filters per gather launch (R and hw copies)
-    f->last_probe_detail = (pg.ring ? PBF_DETAIL_RING : PBF_DETAIL_SORT) | (nfg << 8);
+    f->last_probe_detail = (pg.ring ? PBF_DETAIL_RING : PBF_DETAIL_SORT) | (nf << 8);
     HIP_TRY(sc->regions.ensure(size_t(pg.G) * B * pg.cap * 4));
     HIP_TRY(sc->fill.ensure(size_t(pg.G) * B * 4));
-    // sort partition: per-sub-chunk tile counts; ring partition: cumulative counts per 4 sub-chunks
-    HIP_TRY(sc->subcnt.ensure(pg.ring ? size_t(pg.G) * B * (pg.nq + 1) * 4 : size_t(pg.G) * pg.nsub * B * 4));
+    // both partitions: in-region counts at every 4096-key group boundary
+    HIP_TRY(sc->pref.ensure(size_t(pg.G) * B * (pg.nq + 1) * 2));  // u16 (cap < 2^16)
     const size_t r_words = size_t(pg.G) * B * (pg.cap / 32);
-    HIP_TRY(sc->rbits.ensure(r_words * 4 * nfg));
+    HIP_TRY(sc->rbits.ensure(r_words * 4 * nf));
     const uint64_t neg_words = (b.n + 31) / 32;
     const size_t neg_bytes = neg_words * 4;
     HIP_TRY(sc->neg.ensure(neg_bytes * nf));
     auto* regions = static_cast<uint32_t*>(sc->regions.p);
     auto* fill = static_cast<uint32_t*>(sc->fill.p);
-    auto* subcnt = static_cast<uint32_t*>(sc->subcnt.p);
+    auto* pref = static_cast<uint16_t*>(sc->pref.p);
     auto* R = static_cast<uint32_t*>(sc->rbits.p);
     auto* neg = static_cast<uint32_t*>(sc->neg.p);
     hipStream_t s = f->stream;
     // gather split over S tile ranges (several small workgroups per CU)
     const uint32_t S = pl.gsplit;
-    const bool use_hw = S > 1 || nfg > 1;
+    const bool use_hw = S > 1 || nf > 1;
     uint32_t* hw = nullptr;
     if (use_hw) {
-        HIP_TRY(sc->hw.ensure(neg_bytes * nfg));
+        HIP_TRY(sc->hw.ensure(neg_bytes * nf));
         hw = static_cast<uint32_t*>(sc->hw.p);
     }
     ProbeSet ps{};
@@ -859,8 +860,7 @@ int run_tiled_probe_set(pbf_filter_t* f, pbf_filter_t* const* fs, uint32_t nf, c
     auto tprobe = expand ? k_tile_probe<true> : k_tile_probe<false>;
     auto tprobe_set = expand ? k_tile_probe_set<true> : k_tile_probe_set<false>;
     HIP_TRY(allow_lds(tprobe, lds_tile));
-    // the ring partition zeroes neg (and presets hw for the fused gather) itself
-    if (!pg.ring) HIP_TRY(hipMemsetAsync(neg, 0, neg_bytes * nf, s));
+    // the partition zeroes neg (and presets hw for the gather) itself
     hipError_t err = hipSuccess;
     dispatch(kmax_for(k), b.km, [&](auto KMAX, auto KM) {
         if constexpr (decltype(KMAX)::value > 0) {
@@ -870,7 +870,7 @@ int run_tiled_probe_set(pbf_filter_t* f, pbf_filter_t* const* fs, uint32_t nf, c
                     with_ring_kernel<KX, KMD, true>(k, ring_pow2(tm), [&](auto kern) {
                         err = allow_lds(kern, pl.lds_part);
                         if (err == hipSuccess)
-                            kern<<<pg.G, kPartThreads, pl.lds_part, s>>>(b.ks, b.n, int(k), tm, pg, regions, fill, subcnt,
+                            kern<<<pg.G, kPartThreads, pl.lds_part, s>>>(b.ks, b.n, int(k), tm, pg, regions, fill, pref,
                                                                  nullptr, nullptr, ps, use_hw ? hw : nullptr);
                     });
                 }
@@ -878,8 +878,8 @@ int run_tiled_probe_set(pbf_filter_t* f, pbf_filter_t* const* fs, uint32_t nf, c
                 with_part_kernel<KX, KMD, true>(k, [&](auto kern) {
                     err = allow_lds(kern, pl.lds_part);
                     if (err == hipSuccess)
-                        kern<<<pg.G, kPartThreads, pl.lds_part, s>>>(b.ks, b.n, int(k), tm, pg, regions, fill, subcnt,
-                                                             nullptr, nullptr, ps);
+                        kern<<<pg.G, kPartThreads, pl.lds_part, s>>>(b.ks, b.n, int(k), tm, pg, regions, fill, pref,
+                                                             nullptr, nullptr, ps, use_hw ? hw : nullptr);
                 });
             }
         }
@@ -887,41 +887,25 @@ int run_tiled_probe_set(pbf_filter_t* f, pbf_filter_t* const* fs, uint32_t nf, c
     HIP_TRY(err);
     LAUNCHED(f, pg.ring ? "k_part_ring<probe>" : "k_part<probe>");
     const dim3 grid(pg.G, S);
-    if (pg.ring) {
-        auto gring = nf > 1 ? k_gather_ring<kMaxProbeSet> : k_gather_ring<1>;
-        HIP_TRY(allow_lds(gring, pl.lds_gather));
-        // every filter's tile test (one XCD-aware launch for a set), then ONE gather over the
-        // shared region entries
-        if (nf == 1) {
-            tprobe<<<B, 1024, lds_tile, s>>>(tm, pg, regions, fill, fs[0]->bitmap, R);
-        } else {
-            HIP_TRY(allow_lds(tprobe_set, lds_tile));
-            const uint32_t tgrid = ((B + 7) / 8) * 8 * nf;
-            tprobe_set<<<tgrid, 1024, lds_tile, s>>>(tm, pg, regions, fill, ps, R, r_words);
-        }
-        LAUNCHED(f, nf == 1 ? "k_tile_probe" : "k_tile_probe_set");
-        gring<<<grid, 512, pl.lds_gather, s>>>(tm, pg, b.n, regions, R, fill, subcnt, neg, hitmasks[0] + hm_off, hw, nf,
-                                              r_words, neg_words, pl.gtq);
-        LAUNCHED(f, "k_gather_ring");
-        if (use_hw) {
-            for (uint32_t i = 0; i < nf; ++i) {
-                k_hw_to_hitmask<<<grid_for(neg_words, 256, 4096), 256, 0, s>>>(hw + i * neg_words, b.n,
-                                                                               hitmasks[i] + hm_off);
-                LAUNCHED(f, "k_hw_to_hitmask");
-            }
-        }
-        return PBF_OK;
+    auto gather = nf > 1 ? k_gather_ring<kMaxProbeSet> : k_gather_ring<1>;
+    HIP_TRY(allow_lds(gather, pl.lds_gather));
+    // every filter's tile test (one XCD-aware launch for a set), then ONE gather over the shared
+    // region entries
+    if (nf == 1) {
+        tprobe<<<B, 1024, lds_tile, s>>>(tm, pg, regions, fill, fs[0]->bitmap, R);
+    } else {
+        HIP_TRY(allow_lds(tprobe_set, lds_tile));
+        const uint32_t tgrid = ((B + 7) / 8) * 8 * nf;
+        tprobe_set<<<tgrid, 1024, lds_tile, s>>>(tm, pg, regions, fill, ps, R, r_words);
     }
-    HIP_TRY(allow_lds(k_gather, pl.lds_gather));
-    for (uint32_t i = 0; i < nf; ++i) {
-        if (S > 1) HIP_TRY(hipMemsetAsync(hw, 0xFF, neg_bytes, s));
-        tprobe<<<B, 1024, lds_tile, s>>>(tm, pg, regions, fill, fs[i]->bitmap, R);
-        LAUNCHED(f, "k_tile_probe");
-        k_gather<<<grid, 512, pl.lds_gather, s>>>(tm, pg, b.n, regions, R, subcnt, neg + i * neg_words,
-                                                  hitmasks[i] + hm_off, hw);
-        LAUNCHED(f, "k_gather");
-        if (S > 1) {
-            k_hw_to_hitmask<<<grid_for(neg_words, 256, 4096), 256, 0, s>>>(hw, b.n, hitmasks[i] + hm_off);
+    LAUNCHED(f, nf == 1 ? "k_tile_probe" : "k_tile_probe_set");
+    gather<<<grid, 512, pl.lds_gather, s>>>(tm, pg, b.n, regions, R, fill, pref, neg, hitmasks[0] + hm_off, hw, nf,
+                                           r_words, neg_words, pl.gtq);
+    LAUNCHED(f, "k_gather_ring");
+    if (use_hw) {
+        for (uint32_t i = 0; i < nf; ++i) {
+            k_hw_to_hitmask<<<grid_for(neg_words, 256, 4096), 256, 0, s>>>(hw + i * neg_words, b.n,
+                                                                           hitmasks[i] + hm_off);
             LAUNCHED(f, "k_hw_to_hitmask");
         }
     }
@@ -962,7 +946,8 @@ bool want_tiled_probe(pbf_filter_t* f, uint64_t n) {
 }
 
 // Largest probe batch one tiled pipeline takes: the gather keeps a u16 run-boundary table
-// (B x (nsub+1)) and a bit per key of its workgroup in LDS, and positions stay u32.
+// (B x (nq+1), one row per 4096-key group) and a bit per key of its workgroup in LDS, and
+// positions stay u32.
 uint64_t tiled_probe_batch(pbf_filter_t* f, int km, uint32_t nf = 1) {
     const uint32_t k = f->k;
     uint64_t n = std::max<uint64_t>(64, (kMaxPositions / k) & ~uint64_t(63));
@@ -1808,7 +1793,7 @@ int pbf_scratch_bytes(int device, uint64_t* out) {
     std::lock_guard<std::mutex> lock(pool.mu);
     uint64_t t = 0;
     for (Scratch* sc : pool.sets)
-        for (const DevBuf* d : {&sc->regions, &sc->fill, &sc->ovf, &sc->ovf_count, &sc->subcnt, &sc->rbits, &sc->neg, &sc->hw, &sc->dkeys, &sc->doffs, &sc->dout, &sc->svals, &sc->splan,
+        for (const DevBuf* d : {&sc->regions, &sc->fill, &sc->ovf, &sc->ovf_count, &sc->pref, &sc->rbits, &sc->neg, &sc->hw, &sc->dkeys, &sc->doffs, &sc->dout, &sc->svals, &sc->splan,
                                 &sc->ssec, &sc->serr})
             t += d->bytes;
     *out = t;

@@ -64,7 +64,7 @@ __device__ __forceinline__ uint32_t ring_pos(uint32_t h, const TileMap& tm) {
 template <int KMAX, int KM, bool PROBE, bool POW2, bool EXACT>
 __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k, TileMap tm, PartGeom pg,
                                                     uint32_t* __restrict__ regions, uint32_t* __restrict__ fill,
-                                                    uint32_t* __restrict__ pref, uint32_t* __restrict__ ovf,
+                                                    uint16_t* __restrict__ pref, uint32_t* __restrict__ ovf,
                                                     uint32_t* __restrict__ ovf_count, ProbeSet ps,
                                                     uint32_t* __restrict__ hw_init) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
@@ -220,7 +220,7 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
                 if (b < B) {
                     ht[b] = ((h + ng * GS) << 16) | t;
                     if constexpr (PROBE)
-                        if (((j + 1) & 3) == 0) pref[(uint64_t(g) * nqs + ((j + 1) >> 2)) * B + b] = t;
+                        if (((j + 1) & 3) == 0) pref[(uint64_t(g) * nqs + ((j + 1) >> 2)) * B + b] = uint16_t(t);
                 }
             }
         }
@@ -262,7 +262,7 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
         const uint32_t t = ht[b] & 0xFFFFu;
         fill[uint64_t(b) * pg.G + g] = t;
         if constexpr (PROBE)
-            for (uint32_t q = (j + 3) >> 2; q <= pg.nq; ++q) pref[(uint64_t(g) * nqs + q) * B + b] = t;
+            for (uint32_t q = (j + 3) >> 2; q <= pg.nq; ++q) pref[(uint64_t(g) * nqs + q) * B + b] = uint16_t(t);
     }
 }
 
@@ -285,7 +285,7 @@ template <int NFM>
 __global__ void __launch_bounds__(512) k_gather_ring(TileMap tm, PartGeom pg, uint64_t n,
                                                      const uint32_t* __restrict__ regions,
                                                      const uint32_t* __restrict__ R, const uint32_t* __restrict__ fill,
-                                                     const uint32_t* __restrict__ pref,
+                                                     const uint16_t* __restrict__ pref,
                                                      const uint32_t* __restrict__ neg, uint8_t* __restrict__ hitmask,
                                                      uint32_t* __restrict__ hw, uint32_t nf, uint64_t r_stride,
                                                      uint64_t neg_stride, uint32_t tq) {
@@ -305,7 +305,7 @@ __global__ void __launch_bounds__(512) k_gather_ring(TileMap tm, PartGeom pg, ui
     uint32_t* kbits = smem;                                         // nf x kw words
     uint16_t* lpref = reinterpret_cast<uint16_t*>(kbits + nf * kw);  // nb * nqs (values <= cap < 2^16)
     uint8_t* qtab = reinterpret_cast<uint8_t*>(lpref + ((nb * nqs + 1) & ~1u));  // nb * tq (tq > 0)
-    const uint32_t* gp = pref + uint64_t(g) * nqs * B;  // [q][b] in memory, [b][q] in LDS
+    const uint16_t* gp = pref + uint64_t(g) * nqs * B;  // [q][b] in memory, [b][q] in LDS
     // workgroup g's regions and result words; offsets within them fit 32 bits (B * cap < 2^32)
     const uint32_t* const rgn = regions + uint64_t(g) * B * cap;
     const uint32_t* const Rg = R + uint64_t(g) * B * wpr;
@@ -313,7 +313,7 @@ __global__ void __launch_bounds__(512) k_gather_ring(TileMap tm, PartGeom pg, ui
     auto rword = [&](uint32_t f, uint32_t b, uint32_t r) { return Rg[f * r_stride + (b * wpr + (r >> 5))]; };
     for (uint32_t x = tid; x < nb * nqs; x += nt) {
         const uint32_t q = x / nb, bb = x - q * nb;
-        lpref[bb * nqs + q] = uint16_t(gp[uint64_t(q) * B + b_lo + bb]);
+        lpref[bb * nqs + q] = gp[uint64_t(q) * B + b_lo + bb];
     }
     if (tq) {
         lds_barrier();
@@ -367,8 +367,8 @@ __global__ void __launch_bounds__(512) k_gather_ring(TileMap tm, PartGeom pg, ui
                     const uint32_t r = r0 + lane * 4;
                     uint32_t a = 0;
                     if (b < b_hi && r < fillb[u]) {
-                        // the quad's 4 result bits sit at bits 0, 8, 16, 24 after the shift (see
-                        // r_quad); entries past the fill masked off, no compaction needed here
+                        // the quad's 4 result bits sit at bits 0, 8, 16, 24 after the shift (the R
+                        // layout, tiled_kernels.hpp); entries past the fill masked off
                         const uint32_t cnt = min(fillb[u] - r, 4u);
                         a = (~rw[0][u] >> ((r & 31) >> 2)) & (0x01010101u >> (32 - 8 * cnt));
                     }
@@ -395,7 +395,7 @@ __global__ void __launch_bounds__(512) k_gather_ring(TileMap tm, PartGeom pg, ui
                 const uint32_t r = r0 + lane * 4;
                 if (anyq[u] && b < b_hi && r < fillb[u]) {
                     // failed entries as byte-spread bits: entry r + t at bit 8t (the result word
-                    // shifted to the quad's piece, see r_quad; no compaction multiply)
+                    // shifted to the quad's piece; no compaction multiply)
                     const uint32_t lim = 0x01010101u >> (32 - 8 * min(fillb[u] - r, 4u));
                     uint32_t fl[NFM], any = 0;
 #pragma unroll
@@ -430,7 +430,7 @@ __global__ void __launch_bounds__(512) k_gather_ring(TileMap tm, PartGeom pg, ui
                                     while (lo + 1 < nqs && pb[lo + 1] <= r + t) ++lo;
                                     nxt = lo + 1 < nqs ? uint32_t(pb[lo + 1]) : 0xFFFFFFFFu;
                                 }
-                                // key = (4 lo + (j & 3)) * 1024 + slot = lo << 12 | the entry's top 12 bits
+                                // key = 4096 lo + key-in-group (the entry's top 12 bits)
                                 const uint32_t key = (lo << 12) + (vv[t] >> kSlotShift);
 #pragma unroll
                                 for (int f = 0; f < NFM; ++f)
@@ -445,8 +445,10 @@ __global__ void __launch_bounds__(512) k_gather_ring(TileMap tm, PartGeom pg, ui
     lds_barrier();
     if (S > 1 || nf > 1) {
         for (uint32_t f = 0; f < nf; ++f)
-            for (uint32_t w = tid; w * 32 < nkeys; w += nt)
-                atomicAnd(hw + f * neg_stride + (k0 >> 5) + w, kbits[f * kw + w]);
+            for (uint32_t w = tid; w * 32 < nkeys; w += nt) {
+                const uint32_t bits = kbits[f * kw + w];
+                if (bits != ~0u) atomicAnd(hw + f * neg_stride + (k0 >> 5) + w, bits);  // (hw preset to ones)
+            }
         return;
     }
     for (uint32_t w = tid; w * 32 < nkeys; w += nt) {

@@ -18,14 +18,16 @@
 //         k_tile_build   one workgroup per tile: OR the tile's positions into LDS, write the
 //                        tile once (128 KiB, coalesced).
 //         k_ovf_build    global atomicOr of overflow positions (usually none).
-// Probe:  k_part<probe>  same partition; an entry is (slot-in-sub-chunk << 20 | position in
-//                        tile), and the per-sub-chunk tile counts are kept (subcnt).
+// Probe:  k_part<probe>  same partition; an entry is (key-in-group << 20 | position in tile)
+//                        (a group = 4096 consecutive keys of the workgroup), and the in-region
+//                        counts at every group boundary are kept (pref) — the ring
+//                        partition's format, so both partitions share one gather.
 //         k_tile_probe   one workgroup per tile: load the bitmap tile into LDS, test every
 //                        entry, write one result bit per entry (R, parallel to regions).
-//         k_gather       workgroup g replays its sub-chunks: AND the result bits per key
-//                        in LDS, wave64 ballot → hit-mask words.
+//         k_gather_ring  (ring_kernels.hpp) workgroup g replays its regions: a failed entry
+//                        clears its key's bit in an LDS bitmap, wave64 ballot → hit-mask words.
 //         Overflowed probe entries are tested directly against the bitmap inside k_part; a
-//         miss sets the key's bit in `neg`, which k_gather folds in.
+//         miss sets the key's bit in `neg`, which the gather folds in.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -121,8 +123,8 @@ struct PartGeom {
     uint32_t ring;     // ring partition: LDS ring entries per tile (0 = counting-sort partition)
 };
 
-constexpr uint32_t kSlotShift = 20;   // probe entry = slot-in-sub-chunk << 20 | position in tile
-constexpr uint32_t kSlotMask = 0xFFFu;  // <= 4096 keys per probe sub-chunk
+constexpr uint32_t kSlotShift = 20;   // probe entry = key-in-group << 20 | position in tile
+constexpr uint32_t kGroupKeys = 4096;  // keys per probe group (12 bits of the entry)
 
 __device__ __forceinline__ uint32_t tile_pos(uint32_t h, const TileMap& tm) {
     return tm.cspace ? h : uint32_t(py_index(h, tm.im));
@@ -217,9 +219,9 @@ __host__ __device__ constexpr int part_kpt(int kmax, int km, bool probe) {
 template <int KMAX, int KM, bool PROBE, bool EXACT = false>
 __global__ void __launch_bounds__(kPartThreads) k_part(KeySet ks, uint64_t n, int k, TileMap tm, PartGeom pg,
                                                        uint32_t* __restrict__ regions, uint32_t* __restrict__ fill,
-                                                       uint32_t* __restrict__ subcnt, uint32_t* __restrict__ ovf,
-                                                       uint32_t* __restrict__ ovf_count,
-                                                       ProbeSet ps) {
+                                                       uint16_t* __restrict__ pref, uint32_t* __restrict__ ovf,
+                                                       uint32_t* __restrict__ ovf_count, ProbeSet ps,
+                                                       uint32_t* __restrict__ hw_init) {
     constexpr int KPT = part_kpt(KMAX, KM, PROBE);
     extern __shared__ uint32_t smem[];
     if constexpr (EXACT) k = KMAX;
@@ -234,9 +236,26 @@ __global__ void __launch_bounds__(kPartThreads) k_part(KeySet ks, uint64_t n, in
     uint32_t* stage = ws + 16;         // kps * k
     uint16_t* bkt = reinterpret_cast<uint16_t*>(stage + pg.kps * uint32_t(k));  // kps * k (probes)
     const uint32_t lmask = (1u << tm.tb) - 1u;
-    for (uint32_t b = tid; b < B; b += nt) cursor[b] = 0;
+    // probes: sub-chunks per 4096-key group (kps is 1024, 2048 or 4096 for probes) and the
+    // group-boundary counts pref[g][q][b] (q = 0..nq, b fastest), as the ring partition keeps them
+    const uint32_t spg = kGroupKeys / pg.kps, nqs = pg.nq + 1;
+    for (uint32_t b = tid; b < B; b += nt) {
+        cursor[b] = 0;
+        if constexpr (PROBE) pref[uint64_t(g) * nqs * B + b] = 0;
+    }
     const uint64_t k0 = uint64_t(g) * pg.kpw;
     const uint64_t k1 = min(n, k0 + pg.kpw);
+    if constexpr (PROBE) {
+        // this workgroup's words of every filter's miss bits start at 0 and its gather words
+        // (hw_init) at all ones (as k_part_ring)
+        for (uint64_t w = (k0 >> 5) + tid; w < ((k1 + 31) >> 5); w += nt) {
+            for (uint32_t f = 0; f < ps.nf; ++f) {
+                ps.neg[f * ps.neg_stride + w] = 0u;
+                if (hw_init) hw_init[f * ps.neg_stride + w] = ~0u;
+            }
+        }
+        __syncthreads();  // before any spill of this workgroup ORs into neg
+    }
     // fixed 16-byte keys: the next sub-chunk's keys are loaded during this one's write-out
     uint4 kw[KM == kFixed16 ? KPT : 1];
     auto load_keys = [&](uint64_t s0) {
@@ -274,11 +293,9 @@ __global__ void __launch_bounds__(kPartThreads) k_part(KeySet ks, uint64_t n, in
             }
         }
         lds_barrier();
-        if constexpr (PROBE) {
-            uint32_t* sc = subcnt + (uint64_t(g) * pg.nsub + j) * B;
-            for (uint32_t b = tid; b < B; b += nt) sc[b] = cnt[b];
-        }
         block_exclusive_scan(cnt, lbase, B, ws);
+        // the key's place in its 4096-key group
+        const uint32_t gkey0 = (j & (spg - 1)) * pg.kps;
 #pragma unroll
         for (int u = 0; u < KPT; ++u) {
             const uint32_t slot_key = u * nt + tid;
@@ -288,7 +305,7 @@ __global__ void __launch_bounds__(kPartThreads) k_part(KeySet ks, uint64_t n, in
                     if (s < k) {
                         const uint32_t p = pos[u * KMAX + s];
                         const uint32_t slot = lbase[p >> tm.tb] + rk[u * KMAX + s];
-                        stage[slot] = PROBE ? ((slot_key << kSlotShift) | (p & lmask)) : p;
+                        stage[slot] = PROBE ? (((gkey0 + slot_key) << kSlotShift) | (p & lmask)) : p;
                         if constexpr (PROBE) bkt[slot] = uint16_t(p >> tm.tb);
                     }
                 }
@@ -319,7 +336,8 @@ __global__ void __launch_bounds__(kPartThreads) k_part(KeySet ks, uint64_t n, in
                     if (r < pg.cap) {
                         regions[region_id(g, b[u], pg.G, B) * pg.cap + r] = v[u];
                     } else if constexpr (PROBE) {
-                        spill_probe(ps, pos_to_bit((b[u] << tm.tb) | (v[u] & lmask), tm), s0 + (v[u] >> kSlotShift));
+                        spill_probe(ps, pos_to_bit((b[u] << tm.tb) | (v[u] & lmask), tm),
+                                    s0 + ((v[u] >> kSlotShift) & (pg.kps - 1)));
                     } else {
                         ovf[atomicAdd(ovf_count, 1u)] = v[u];
                     }
@@ -327,13 +345,20 @@ __global__ void __launch_bounds__(kPartThreads) k_part(KeySet ks, uint64_t n, in
             }
         }
         lds_barrier();
-        for (uint32_t b = tid; b < B; b += nt) cursor[b] += lbase[b + 1];
+        // a group ends after this sub-chunk: its boundary count (same thread reads cursor[b])
+        const bool gend = PROBE && ((j + 1) & (spg - 1)) == 0;
+        for (uint32_t b = tid; b < B; b += nt) {
+            const uint32_t c = cursor[b] + lbase[b + 1];
+            cursor[b] = c;
+            if (gend) pref[(uint64_t(g) * nqs + ((j + 1) / spg)) * B + b] = uint16_t(min(c, pg.cap));
+        }
     }
     lds_barrier();
     for (uint32_t b = tid; b < B; b += nt) {
-        fill[uint64_t(b) * pg.G + g] = min(cursor[b], pg.cap);
-        if constexpr (PROBE)  // the last workgroup may run fewer than nsub sub-chunks
-            for (uint32_t jj = j; jj < pg.nsub; ++jj) subcnt[(uint64_t(g) * pg.nsub + jj) * B + b] = 0;
+        const uint32_t t = min(cursor[b], pg.cap);
+        fill[uint64_t(b) * pg.G + g] = t;
+        if constexpr (PROBE)  // the open last group and any the workgroup did not reach
+            for (uint32_t q = (j + spg - 1) / spg; q <= pg.nq; ++q) pref[(uint64_t(g) * nqs + q) * B + b] = uint16_t(t);
     }
 }
 
@@ -449,15 +474,6 @@ __global__ void __launch_bounds__(256) k_ovf_build(TileMap tm, const uint32_t* _
 // Result bits R: one 32-bit word per 32-entry word of a region, bit (8t + l) = entry 4l + t
 // (l = the entry's 16-byte piece of the word, t = its place in the piece).  This is the layout
 // four wave ballots produce when 8 lanes read a word piece by piece (k_tile_probe).
-// r_quad: the 4 result bits of the piece holding entries r..r+3 (r % 4 == 0).
-// The four bits sit at l, 8+l, 16+l, 24+l; after the shift and mask, one multiply by 0x01020408
-// moves byte t's bit to bit 24+t (the other partial products land below bit 24 or above bit 31,
-// each on its own bit, so nothing carries into 24..27).
-__device__ __forceinline__ uint32_t r_quad(uint32_t rw, uint32_t r) {
-    const uint32_t x = (rw >> ((r & 31) >> 2)) & 0x01010101u;
-    return (x * 0x01020408u) >> 24;
-}
-
 // One workgroup per tile.  Region words are read 8 per wave instruction: lane = one 16-byte
 // piece of a word, so an instruction reads 1 KiB contiguously (words are consecutive within a
 // region).  Each lane tests its 4 entries in the LDS tile; four ballots give every word's 32
@@ -571,130 +587,6 @@ __global__ void __launch_bounds__(1024) k_tile_probe_set(TileMap tm, PartGeom pg
     if (b >= tm.nbuckets) return;
     // the set's other workgroups of tile b read the same lines: temporal loads keep them in L2
     tile_probe_body<false, EXPAND>(smem, b, tm, pg, regions, fill, ps.bm[f], R + f * r_stride);
-}
-
-// Workgroup g owns keys [g*kpw, (g+1)*kpw) and regions (g, 0..B-1).  It reads each region once,
-// contiguously, with its result bits; an entry's sub-chunk j follows from the region's run
-// boundaries (prefix over j of the in-region counts, from subcnt), and its key is
-// g*kpw + j*kps + slot.  A 0 result bit clears the key's bit in an LDS bitmap of the
-// workgroup's keys, which is finally written out as hit-mask words.
-//   LDS: pref[B][nsub+1] (u16 run boundaries, region-relative), kbits[kpw/32].
-__global__ void __launch_bounds__(512) k_gather(TileMap tm, PartGeom pg, uint64_t n,
-                                                const uint32_t* __restrict__ regions, const uint32_t* __restrict__ R,
-                                                const uint32_t* __restrict__ subcnt, const uint32_t* __restrict__ neg,
-                                                uint8_t* __restrict__ hitmask, uint32_t* __restrict__ hw) {
-    extern __shared__ uint32_t smem[];
-    const uint32_t B = tm.nbuckets, cap = pg.cap, wpr = cap / 32, nsub = pg.nsub;
-    const uint32_t tid = threadIdx.x, nt = blockDim.x;
-    const uint32_t lane = tid & 63, wave = tid >> 6, nwaves = nt >> 6;
-    const uint32_t g = blockIdx.x;
-    // split sp of S takes tiles [b_lo, b_hi) (as k_gather_ring)
-    const uint32_t S = gridDim.y, sp = blockIdx.y;
-    const uint32_t b_lo = uint32_t(uint64_t(B) * sp / S), b_hi = uint32_t(uint64_t(B) * (sp + 1) / S);
-    const uint64_t k0 = uint64_t(g) * pg.kpw;
-    const uint64_t k1 = min(n, k0 + pg.kpw);
-    const uint32_t nkeys = uint32_t(k1 - k0);
-    const uint32_t kw = uint32_t((pg.kpw + 31) / 32);
-    uint32_t* kbits = smem;                                    // kw words
-    uint16_t* pref = reinterpret_cast<uint16_t*>(kbits + kw);  // (b_hi - b_lo) * (nsub + 1)
-    const uint32_t ps = nsub + 1;
-    // key bits: 1 for this workgroup's keys not already refuted by an overflow entry
-    for (uint32_t w = tid; w < kw; w += nt) {
-        const uint32_t key0 = w * 32;
-        uint32_t m = key0 >= nkeys ? 0u : (nkeys - key0 >= 32 ? ~0u : ((1u << (nkeys - key0)) - 1u));
-        if (m) {
-            const uint64_t gk = k0 + key0;  // neg is indexed by batch key; k0 is a multiple of 64
-            m &= ~neg[gk >> 5];
-        }
-        kbits[w] = m;
-    }
-    // run boundaries per tile: pref[b][j] = in-region entries of (g, b) before sub-chunk j
-    const uint32_t* sc = subcnt + uint64_t(g) * nsub * B;
-    for (uint32_t b = b_lo + tid; b < b_hi; b += nt) {
-        uint16_t* pr = pref + (b - b_lo) * ps;
-        uint32_t run = 0;
-        pr[0] = 0;
-        for (uint32_t j0 = 0; j0 < nsub; j0 += 8) {
-            uint32_t c[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) c[u] = j0 + u < nsub ? sc[uint64_t(j0 + u) * B + b] : 0u;
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                if (j0 + u < nsub) {
-                    run = min(run + c[u], cap);
-                    pr[j0 + u + 1] = uint16_t(run);
-                }
-            }
-        }
-    }
-    lds_barrier();
-    // one wave per region, 256 entries (one 16-byte load per lane) per step; U regions in
-    // flight per wave.  Regions start 128-B aligned (cap is a multiple of 32).
-    constexpr int U = 4;
-    for (uint32_t b0 = b_lo + wave; b0 < b_hi; b0 += nwaves * U) {
-        uint32_t fillb[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-            fillb[u] = b0 + u * nwaves < b_hi ? uint32_t(pref[(b0 + u * nwaves - b_lo) * ps + nsub]) : 0u;
-        uint32_t maxf = 0;
-#pragma unroll
-        for (int u = 0; u < U; ++u) maxf = max(maxf, fillb[u]);
-        for (uint32_t r0 = 0; r0 < maxf; r0 += 256) {
-            uint4 v[U];
-            uint32_t rw[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const uint32_t b = min(b0 + u * nwaves, b_hi - 1);
-                const uint32_t r = min(r0 + lane * 4, (max(fillb[u], 1u) - 1) & ~3u);
-                const uint64_t reg = region_id(g, b, pg.G, B);
-                v[u] = ld_stream(regions + reg * cap + r);
-                rw[u] = R[reg * wpr + (r >> 5)];
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const uint32_t b = b0 + u * nwaves;
-                const uint32_t r = r0 + lane * 4;
-                if (b < b_hi && r < fillb[u]) {
-                    uint32_t fails = ~r_quad(rw[u], r) & 0xFu;
-                    if (fillb[u] - r < 4) fails &= (1u << (fillb[u] - r)) - 1u;
-                    if (fails) {
-                        // sub-chunk of position r: the last j with pref[b][j] <= r
-                        const uint16_t* pb = pref + (b - b_lo) * ps;
-                        uint32_t lo = 0, len = nsub;
-                        while (len > 1) {
-                            const uint32_t half = len >> 1;
-                            if (pb[lo + half] <= r) lo += half;
-                            len -= half;
-                        }
-                        const uint32_t vv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-#pragma unroll
-                        for (int t = 0; t < 4; ++t) {
-                            if ((fails >> t) & 1u) {
-                                while (lo + 1 < nsub && pb[lo + 1] <= r + t) ++lo;
-                                const uint32_t key = lo * pg.kps + ((vv[t] >> kSlotShift) & kSlotMask);
-                                atomicAnd(kbits + (key >> 5), ~(1u << (key & 31)));
-                            }
-                        }
-                    }
-                }
-            }
-        }
-    }
-    lds_barrier();
-    if (S > 1) {  // this split's words into hw (k_hw_to_hitmask writes the hit mask)
-        for (uint32_t w = tid; w * 32 < nkeys; w += nt) atomicAnd(hw + (k0 >> 5) + w, kbits[w]);
-        return;
-    }
-    // hit-mask words for keys [k0, k1): k0 is a multiple of 64
-    for (uint32_t w = tid; w * 32 < nkeys; w += nt) {
-        const uint64_t key0 = k0 + uint64_t(w) * 32;
-        const uint32_t bits = kbits[w];
-        const uint64_t nb = min<uint64_t>(4, (n - key0 + 7) / 8);
-        if (nb == 4 && (reinterpret_cast<uintptr_t>(hitmask + key0 / 8) & 3) == 0)
-            *reinterpret_cast<uint32_t*>(hitmask + key0 / 8) = bits;
-        else
-            for (uint64_t q = 0; q < nb; ++q) hitmask[key0 / 8 + q] = uint8_t(bits >> (8 * q));
-    }
 }
 
 // hw (ANDed gather words, one per 32 keys) → the LSB-first hit mask of n keys.
