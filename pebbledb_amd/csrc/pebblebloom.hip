@@ -597,7 +597,7 @@ bool ring_pow2(const TileMap& tm) { return tm.im.mode == kPow2 && !tm.cspace; }
 
 // Keys per sub-chunk of a ring partition of B tiles and k hashes (0 = the ring does not apply):
 // the largest of 1024 / 512 / 256 with kps * k <= B * GS / 2.  Probes keep 1024 (the entry's
-// slot field), builds may take smaller sub-chunks (k = 10 over 1024 tiles: 512).
+// thread field), builds may take smaller sub-chunks (k = 10 over 1024 tiles: 512).
 uint32_t ring_kps(uint32_t B, uint32_t k, bool probe, uint32_t tb) {
     const int ov = part_override();
     if (ov == 1 || k == 0 || k > 16 || B > 1024 || (probe && tb > kSlotShift)) return 0;
@@ -630,7 +630,7 @@ void set_gather(PartPlan& pl, uint32_t B, uint32_t row, uint32_t nf = 1) {
     }
 }
 
-PartPlan plan_ring(uint32_t B, uint32_t k, uint64_t n, uint32_t kps, double share, uint32_t nf = 1) {
+PartPlan plan_ring(uint32_t B, uint32_t k, uint64_t n, uint32_t kps, bool probe, double share, uint32_t nf = 1) {
     PartPlan pl{};
     const uint64_t G0 = std::min<uint64_t>(part_max_groups(false), std::max<uint64_t>(1, (n + kps - 1) / kps));
     uint64_t kpw = (n + G0 - 1) / G0;
@@ -639,12 +639,15 @@ PartPlan plan_ring(uint32_t B, uint32_t k, uint64_t n, uint32_t kps, double shar
     pl.pg.kps = kps;
     pl.pg.kpw = kpw;
     pl.pg.nsub = uint32_t(kpw / kps);
-    pl.pg.nq = (pl.pg.nsub + 3) / 4;
+    pl.pg.nq = uint32_t((kpw + kGroupKeys - 1) / kGroupKeys);
     pl.pg.ring = kRingEntries;
     const double mu = double(kpw) * k * share;
     const uint64_t cap = uint64_t(mu + 8.0 * std::sqrt(mu) + 32.0);
     pl.pg.cap = uint32_t(((cap + 31) / 32) * 32);
-    pl.lds_part = size_t(ring_lds_words(B)) * 4;
+    // the rest of the CU's 160 KiB of LDS (up to 4096 entries) buffers spilled positions
+    const size_t ring_bytes = size_t(ring_lds_words(B)) * 4, spill_entry = probe ? 8 : 4;
+    pl.pg.spill_cap = uint32_t(std::min<size_t>(4096, (160 * 1024 - ring_bytes) / spill_entry));
+    pl.lds_part = ring_bytes + size_t(pl.pg.spill_cap) * spill_entry;
     set_gather(pl, B, pl.pg.nq + 1, nf);
     return pl;
 }
@@ -708,7 +711,7 @@ PartPlan plan_for(const TileMap& tm, uint32_t k, int km, uint64_t n, bool probe,
     const uint32_t B = tm.nbuckets;
     const double share = busiest_tile_share(tm);
     if (const uint32_t kps = ring_kps(B, k, probe, tm.tb)) {
-        const PartPlan pl = plan_ring(B, k, n, kps, share, probe ? nf : 1);
+        const PartPlan pl = plan_ring(B, k, n, kps, probe, share, probe ? nf : 1);
         // head / tail are 16-bit halves in LDS (cap <= 32768); entry offsets within a
         // workgroup's regions are 32-bit (B * cap < 2^32)
         if (pl.pg.cap <= 32768 && uint64_t(B) * pl.pg.cap < (uint64_t(1) << 32)) return pl;

@@ -18,12 +18,17 @@
 //             lands at region position e.
 //   sub-chunk kps keys (<= 1024, one per thread).  The host picks the geometry so a tile receives
 //             <= GS/2 positions per sub-chunk on average; a position that would overrun the ring
-//             (or the region capacity) leaves the stream (build: overflow list; probe: tested
-//             against the bitmap in place, a miss clears the key via `neg`).
-//   probe     entry = (j & 3) << 30 | slot << 20 | position-in-tile (slot = thread, j = sub-chunk).
-//             pref[g][q][b] = in-region entries of (g, b) before sub-chunk 4q (b fastest, so a
-//             wave's stores of 64 tiles are one contiguous 256-B run), so k_gather_ring
-//             finds an entry's sub-chunk from its region position and the entry's j & 3.
+//             (or the region capacity) leaves the stream into an LDS spill buffer, handled once at
+//             the end of the kernel (build: copied to the overflow list; probe: tested against the
+//             bitmap, a miss sets the key's bit in `neg`); past the buffer's capacity it is
+//             handled in place.  (Two 1024-key units per flush — half the barriers and flush
+//             scans per key, ~0.2% of positions spilled — measured slower: C2 build 0.199 ->
+//             0.212 ms, probe neutral, C5 9.35 -> 9.55 ms; profiles/r03/s7.)
+//   probe     entry = key-in-group << 20 | position-in-tile, key-in-group = (j & 3) << 10 |
+//             thread (j = sub-chunk; a group = 4096 keys = 4 sub-chunks of 1024).  pref[g][q][b] = in-region entries
+//             of (g, b) before group q (b fastest, so a wave's stores of 64 tiles are one
+//             contiguous 256-B run), so k_gather_ring finds an entry's group from its region
+//             position.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -32,18 +37,19 @@
 
 namespace pbf {
 
-constexpr uint32_t kRingKeysPerSub = 1024;  // = threads; slot field is 10 bits
+constexpr uint32_t kRingKeysPerSub = 1024;  // = threads; the thread field is 10 bits
 constexpr uint32_t kRingEntries = 32;       // RC: LDS ring entries per tile (64-B groups of 16)
-static_assert(kSlotShift == 20 && kRingKeysPerSub == 1024, "ring entry = (j & 3) << 30 | slot << 20 | position");
+static_assert(kSlotShift == 20 && kRingKeysPerSub == 1024 && kGroupKeys == 4 * kRingKeysPerSub,
+              "probe entry = ((j & 3) << 10 | thread) << 20 | position");
 // Key sub-chunks loaded per batch, one batch ahead: 2 measured best with the non-temporal streams
 // (C2 A/B over 1/2/3/4/8: profiles/r01/s11/ab.txt)
 constexpr int kRingPrefetch = 2;
 constexpr uint32_t kRingDescPerWave = 128;  // flush descriptors per wave (64 tiles x <= 2 groups)
 
 // LDS layout of k_part_ring (u32 words): head|tail per tile [B], flush descriptors [16 waves x
-// 128], one dump word (appends that left the stream write there), then the rings [B x RC],
-// 16-B aligned.
-__host__ __device__ constexpr uint32_t ring_lds_base(uint32_t B) { return (B + 16 * kRingDescPerWave + 1 + 3) & ~3u; }
+// 128], one dump word (appends that left the stream write there), the spill count, then the rings
+// [B x RC], 16-B aligned, then the spill buffer (probe: 2 words per entry, build: 1).
+__host__ __device__ constexpr uint32_t ring_lds_base(uint32_t B) { return (B + 16 * kRingDescPerWave + 2 + 3) & ~3u; }
 __host__ __device__ constexpr uint32_t ring_lds_words(uint32_t B) { return ring_lds_base(B) + B * kRingEntries; }
 
 // Tile position of a hash when m is a power of two <= 2^32 (POW2) or in general.
@@ -70,6 +76,7 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     if constexpr (EXACT) k = KMAX;
     constexpr uint32_t RC = kRingEntries, GS = RC / 2, rmask = RC - 1;
+    constexpr uint32_t SW = PROBE ? 2 : 1;  // spill-buffer words per entry
     const uint32_t B = tm.nbuckets;
     const uint32_t shift = tm.tb;
     const uint32_t kps = pg.kps;  // keys per sub-chunk (<= 1024 threads)
@@ -81,9 +88,11 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
     // ht[b] = head << 16 | tail: one LDS atomic add appends a position and returns the tile's
     // flush cursor with its slot (no separate head read per position)
     uint32_t* const ht = smem;
-    uint32_t* const desc = smem + B;                        // 16 waves x 128 group descriptors
+    uint32_t* const desc = smem + B;                  // 16 waves x 128 group descriptors
     const uint32_t dump = B + 16 * kRingDescPerWave;  // word index of the dump slot
-    uint32_t* const ring = smem + ring_lds_base(B);          // B * RC, 16-B aligned
+    uint32_t* const nspill = smem + dump + 1;
+    uint32_t* const ring = smem + ring_lds_base(B);   // B * RC, 16-B aligned
+    uint32_t* const sbuf = ring + B * RC;             // pg.spill_cap entries
     // this workgroup's regions; an entry's offset in them fits 32 bits (B * cap < 2^32), and
     // tb < 4096, cap < 2^20 make it one 24-bit multiply-add
     uint32_t* const rgn = regions + uint64_t(g) * B * cap;
@@ -93,6 +102,7 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
         ht[b] = 0;
         if constexpr (PROBE) pref[uint64_t(g) * nqs * B + b] = 0;
     }
+    if (tid == 0) *nspill = 0;
     const uint64_t k0 = uint64_t(g) * pg.kpw;
     const uint64_t k1 = min(n, k0 + pg.kpw);
     if constexpr (PROBE) {
@@ -118,8 +128,21 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
             }
         }
     };
+    // A position that leaves the stream (its ring or region is full): into the spill buffer, or
+    // past its capacity handled here (build: overflow list; probe: tested now).
+    auto spill_one = [&](uint32_t p, uint64_t i) {
+        const uint32_t x = atomicAdd(nspill, 1u);
+        if (x < pg.spill_cap) {
+            sbuf[x * SW] = p;
+            if constexpr (PROBE) sbuf[x * SW + 1] = uint32_t(i - k0);
+        } else if constexpr (PROBE) {
+            spill_probe(ps, pos_to_bit(p, tm), i);
+        } else {
+            ovf[atomicAdd(ovf_count, 1u)] = p;
+        }
+    };
     load_batch(k0);
-    uint32_t j = 0;
+    uint32_t j = 0;  // sub-chunks done
     for (uint64_t c0 = k0; c0 < k1; c0 += uint64_t(P) * kps) {
         uint4 cw[F16 ? P : 1];
         if constexpr (F16) {
@@ -167,17 +190,10 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
                         spill |= uint32_t(!ok) << s;
                     }
                 }
-                if (spill) {  // rare (heavy key duplication): out of the stream
+                if (spill) {  // rare: heavy key duplication
 #pragma unroll
-                    for (int s = 0; s < KMAX; ++s) {
-                        if ((spill >> s) & 1u) {
-                            if constexpr (PROBE) {  // test this position here
-                                spill_probe(ps, pos_to_bit(pos[s], tm), i);
-                            } else {
-                                ovf[atomicAdd(ovf_count, 1u)] = pos[s];
-                            }
-                        }
-                    }
+                    for (int s = 0; s < KMAX; ++s)
+                        if ((spill >> s) & 1u) spill_one(pos[s], i);
                 }
             }
             lds_barrier();
@@ -263,6 +279,19 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
         fill[uint64_t(b) * pg.G + g] = t;
         if constexpr (PROBE)
             for (uint32_t q = (j + 3) >> 2; q <= pg.nq; ++q) pref[(uint64_t(g) * nqs + q) * B + b] = uint16_t(t);
+    }
+    // the buffered spills (every append is done: the barrier above)
+    const uint32_t ns = min(*nspill, pg.spill_cap);
+    if (ns) {
+        if constexpr (PROBE) {
+            for (uint32_t x = tid; x < ns; x += nt) spill_probe(ps, pos_to_bit(sbuf[2 * x], tm), k0 + sbuf[2 * x + 1]);
+        } else {
+            lds_barrier();  // every thread has read nspill before the dump word takes the base
+            if (tid == 0) smem[dump] = atomicAdd(ovf_count, ns);
+            lds_barrier();
+            const uint32_t base = smem[dump];
+            for (uint32_t x = tid; x < ns; x += nt) ovf[base + x] = sbuf[x];
+        }
     }
 }
 
@@ -419,22 +448,35 @@ __global__ void __launch_bounds__(512) k_gather_ring(TileMap tm, PartGeom pg, ui
                             }
                         }
                         const uint32_t vv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-                        // the next group's first entry: a boundary inside the quad is rare (a
-                        // group holds ~24 entries at C2), so entries usually take lo with one compare
-                        uint32_t nxt = lo + 1 < nqs ? uint32_t(pb[lo + 1]) : 0xFFFFFFFFu;
+                        // the next two groups' first entries: with no second boundary inside the
+                        // quad (nearly always: a group holds ~24 entries of a region at C2) an
+                        // entry's group is lo or lo + 1 by one compare, no loop
+                        const uint32_t nxt1 = lo + 1 < nqs ? uint32_t(pb[lo + 1]) : 0xFFFFFFFFu;
+                        const uint32_t nxt2 = lo + 2 < nqs ? uint32_t(pb[lo + 2]) : 0xFFFFFFFFu;
+                        if (nxt2 > r + 3) {
 #pragma unroll
-                        for (int t = 0; t < 4; ++t) {
-                            if ((any >> (8 * t)) & 1u) {
-                                if (r + t >= nxt) {
-                                    ++lo;
-                                    while (lo + 1 < nqs && pb[lo + 1] <= r + t) ++lo;
-                                    nxt = lo + 1 < nqs ? uint32_t(pb[lo + 1]) : 0xFFFFFFFFu;
-                                }
-                                // key = 4096 lo + key-in-group (the entry's top 12 bits)
-                                const uint32_t key = (lo << 12) + (vv[t] >> kSlotShift);
+                            for (int t = 0; t < 4; ++t) {
+                                // key = 4096 group + key-in-group (the entry's top 12 bits)
+                                const uint32_t key = ((lo + uint32_t(r + t >= nxt1)) << 12) + (vv[t] >> kSlotShift);
 #pragma unroll
                                 for (int f = 0; f < NFM; ++f)
                                     if ((fl[f] >> (8 * t)) & 1u) atomicAnd(kbits + f * kw + (key >> 5), ~(1u << (key & 31)));
+                            }
+                        } else {
+                            uint32_t nxt = nxt1;
+#pragma unroll
+                            for (int t = 0; t < 4; ++t) {
+                                if ((any >> (8 * t)) & 1u) {
+                                    if (r + t >= nxt) {
+                                        ++lo;
+                                        while (lo + 1 < nqs && pb[lo + 1] <= r + t) ++lo;
+                                        nxt = lo + 1 < nqs ? uint32_t(pb[lo + 1]) : 0xFFFFFFFFu;
+                                    }
+                                    const uint32_t key = (lo << 12) + (vv[t] >> kSlotShift);
+#pragma unroll
+                                    for (int f = 0; f < NFM; ++f)
+                                        if ((fl[f] >> (8 * t)) & 1u) atomicAnd(kbits + f * kw + (key >> 5), ~(1u << (key & 31)));
+                                }
                             }
                         }
                     }

@@ -119,8 +119,10 @@ struct PartGeom {
     uint32_t kps;      // keys per sub-chunk (kpt * 1024; <= 4096 for probes)
     uint32_t nsub;     // sub-chunks per workgroup
     uint64_t kpw;      // keys per workgroup (= nsub * kps)
-    uint32_t nq;       // ring partition: pref groups (4 sub-chunks each) per workgroup
+    uint32_t nq;       // pref groups (4096 keys each) per workgroup
     uint32_t ring;     // ring partition: LDS ring entries per tile (0 = counting-sort partition)
+    uint32_t spill_cap;  // ring partition: entries of the LDS spill buffer
+    uint32_t pad;
 };
 
 constexpr uint32_t kSlotShift = 20;   // probe entry = key-in-group << 20 | position in tile
@@ -229,9 +231,11 @@ __global__ void __launch_bounds__(kPartThreads) k_part(KeySet ks, uint64_t n, in
     const uint32_t tid = threadIdx.x, nt = blockDim.x;
     const uint32_t kpt = pg.kps / nt;  // <= KPT
     const uint32_t g = blockIdx.x;
-    uint32_t* cursor = smem;           // B: entries routed to (g, b) so far
-    uint32_t* cnt = cursor + B;        // B: this sub-chunk's per-tile count
-    uint32_t* lbase = cnt + B;         // B+1
+    // cb[b] = entries routed to (g, b) before the current sub-chunk - lbase[b] (the write-out's
+    // region position of stage entry e is cb[b] + e)
+    uint32_t* cb = smem;               // B
+    uint32_t* cnt = cb + B;            // B: the next sub-chunk's per-tile count
+    uint32_t* lbase = cnt + B;         // B+1: the current sub-chunk's exclusive scan of its counts
     uint32_t* ws = lbase + B + 1;      // 16
     uint32_t* stage = ws + 16;         // kps * k
     uint16_t* bkt = reinterpret_cast<uint16_t*>(stage + pg.kps * uint32_t(k));  // kps * k (probes)
@@ -240,7 +244,9 @@ __global__ void __launch_bounds__(kPartThreads) k_part(KeySet ks, uint64_t n, in
     // group-boundary counts pref[g][q][b] (q = 0..nq, b fastest), as the ring partition keeps them
     const uint32_t spg = kGroupKeys / pg.kps, nqs = pg.nq + 1;
     for (uint32_t b = tid; b < B; b += nt) {
-        cursor[b] = 0;
+        cb[b] = 0;
+        cnt[b] = 0;
+        lbase[b + 1] = 0;
         if constexpr (PROBE) pref[uint64_t(g) * nqs * B + b] = 0;
     }
     const uint64_t k0 = uint64_t(g) * pg.kpw;
@@ -256,7 +262,7 @@ __global__ void __launch_bounds__(kPartThreads) k_part(KeySet ks, uint64_t n, in
         }
         __syncthreads();  // before any spill of this workgroup ORs into neg
     }
-    // fixed 16-byte keys: the next sub-chunk's keys are loaded during this one's write-out
+    // fixed 16-byte keys: a sub-chunk's keys are loaded one sub-chunk ahead
     uint4 kw[KM == kFixed16 ? KPT : 1];
     auto load_keys = [&](uint64_t s0) {
         if constexpr (KM == kFixed16) {
@@ -267,16 +273,13 @@ __global__ void __launch_bounds__(kPartThreads) k_part(KeySet ks, uint64_t n, in
             }
         }
     };
-    if (k0 < k1) load_keys(k0);
-    uint32_t j = 0;
-    for (uint64_t s0 = k0; s0 < k1; s0 += pg.kps, ++j) {
-        const uint64_t s1 = min(k1, s0 + pg.kps);
-        for (uint32_t b = tid; b < B; b += nt) cnt[b] = 0;
-        lds_barrier();
-        // (initialised so no value stays live across the sub-chunk loop's back-edge)
-        uint32_t pos[KPT * KMAX], rk[KPT * KMAX];
+    // a sub-chunk's positions and their ranks in their tiles (counted into cnt), kept in
+    // registers until the sub-chunk is placed
+    uint32_t pos[KPT * KMAX], rk[KPT * KMAX];
 #pragma unroll
-        for (int e = 0; e < KPT * KMAX; ++e) pos[e] = rk[e] = 0;
+    for (int e = 0; e < KPT * KMAX; ++e) pos[e] = rk[e] = 0;
+    auto hash_count = [&](uint64_t s0) {
+        const uint64_t s1 = min(k1, s0 + pg.kps);
 #pragma unroll
         for (int u = 0; u < KPT; ++u) {
             const uint64_t i = s0 + u * nt + tid;
@@ -292,9 +295,73 @@ __global__ void __launch_bounds__(kPartThreads) k_part(KeySet ks, uint64_t n, in
                     hash_key<KMAX, KM>(ks, i, k, emit);
             }
         }
+    };
+    // Exclusive scan of cnt into lbase (lbase[B] = the sub-chunk's total) that also moves cb past
+    // the previous sub-chunk: cb[b] += lbase_prev[b + 1] - lbase[b] (= its old value + lbase_prev[b]
+    // + its count - lbase[b]); a previous sub-chunk that closed a 4096-key group leaves the
+    // routed count cb[b] + lbase_prev[b + 1] in pref.  A thread scans <= 4 tiles (B <= 4096).
+    // Ends synced.
+    auto scan_advance = [&](bool group_end, uint32_t q) {
+        const uint32_t per = (B + nt - 1) / nt;
+        const uint32_t lo = min(B, tid * per), hi = min(B, lo + per);
+        uint32_t sum = 0, prevn[4];
+#pragma unroll
+        for (int x = 0; x < 4; ++x) {
+            const uint32_t b = lo + x;
+            prevn[x] = 0;
+            if (b < hi) {
+                sum += cnt[b];
+                prevn[x] = lbase[b + 1];
+            }
+        }
+        uint32_t v = sum;
+        const uint32_t lane = tid & 63;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t o = __shfl_up(v, d, 64);
+            if (lane >= uint32_t(d)) v += o;
+        }
+        if (lane == 63) ws[tid >> 6] = v;
         lds_barrier();
-        block_exclusive_scan(cnt, lbase, B, ws);
-        // the key's place in its 4096-key group
+        if (tid < 64) {
+            const uint32_t nw = nt >> 6;
+            uint32_t w = tid < nw ? ws[tid] : 0u;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t o = __shfl_up(w, d, 64);
+                if (tid >= uint32_t(d)) w += o;
+            }
+            if (tid < nw) ws[tid] = w;
+        }
+        lds_barrier();
+        uint32_t run = v - sum + ((tid >> 6) ? ws[(tid >> 6) - 1] : 0u);
+#pragma unroll
+        for (int x = 0; x < 4; ++x) {
+            const uint32_t b = lo + x;
+            if (b < hi) {
+                const uint32_t c = cb[b] + prevn[x];  // routed before this sub-chunk
+                if (PROBE && group_end) pref[(uint64_t(g) * nqs + q) * B + b] = uint16_t(min(c, pg.cap));
+                cb[b] = c - run;
+                lbase[b] = run;
+                run += cnt[b];
+            }
+        }
+        if (tid == nt - 1) lbase[B] = run;
+        lds_barrier();
+    };
+    if (k0 < k1) {
+        load_keys(k0);
+        lds_barrier();  // cnt cleared
+        hash_count(k0);
+        if (k0 + pg.kps < k1) load_keys(k0 + pg.kps);
+    }
+    uint32_t j = 0;
+    for (uint64_t s0 = k0; s0 < k1; s0 += pg.kps, ++j) {
+        const uint64_t s1 = min(k1, s0 + pg.kps);
+        lds_barrier();  // this sub-chunk's counts are complete, the previous write-out is done
+        scan_advance(PROBE && j > 0 && (j & (spg - 1)) == 0, j / spg);
+        // place the sub-chunk's entries, sorted by tile, into the stage (the key's place in its
+        // 4096-key group goes into a probe entry); cnt is free again
         const uint32_t gkey0 = (j & (spg - 1)) * pg.kps;
 #pragma unroll
         for (int u = 0; u < KPT; ++u) {
@@ -311,13 +378,17 @@ __global__ void __launch_bounds__(kPartThreads) k_part(KeySet ks, uint64_t n, in
                 }
             }
         }
-        for (uint32_t b = tid; b < B; b += nt) cursor[b] -= lbase[b];
+        for (uint32_t b = tid; b < B; b += nt) cnt[b] = 0;
         lds_barrier();
-        if (s0 + pg.kps < k1) load_keys(s0 + pg.kps);
-        // Lane-parallel write-out: entry e of the sorted stage goes to position
-        // cursor[b] + (e - lbase[b]) of region (g, b) (cursor pre-biased by -lbase below).
-        // Eight entries per thread per batch, loads unconditional, so each thread has eight
-        // independent LDS → store chains in flight.  Positions >= cap overflow.
+        // The next sub-chunk is hashed and counted while this one is written out: the hash's
+        // VALU work overlaps the write-out's LDS reads and stores (other waves, same phase).
+        if (s1 < k1) {
+            hash_count(s1);
+            if (s1 + pg.kps < k1) load_keys(s1 + pg.kps);
+        }
+        // Lane-parallel write-out: entry e of the sorted stage goes to position cb[b] + e of
+        // region (g, b).  Eight entries per thread per batch, loads unconditional, so each thread
+        // has eight independent LDS → store chains in flight.  Positions >= cap overflow.
         const uint32_t tot = lbase[B];
         constexpr int UW = 8;
         for (uint32_t e0 = tid; e0 < tot; e0 += nt * UW) {
@@ -331,7 +402,7 @@ __global__ void __launch_bounds__(kPartThreads) k_part(KeySet ks, uint64_t n, in
 #pragma unroll
             for (int u = 0; u < UW; ++u) {
                 const uint32_t e = e0 + u * nt;
-                const uint32_t r = cursor[b[u]] + e;
+                const uint32_t r = cb[b[u]] + e;
                 if (e < tot) {
                     if (r < pg.cap) {
                         regions[region_id(g, b[u], pg.G, B) * pg.cap + r] = v[u];
@@ -344,18 +415,10 @@ __global__ void __launch_bounds__(kPartThreads) k_part(KeySet ks, uint64_t n, in
                 }
             }
         }
-        lds_barrier();
-        // a group ends after this sub-chunk: its boundary count (same thread reads cursor[b])
-        const bool gend = PROBE && ((j + 1) & (spg - 1)) == 0;
-        for (uint32_t b = tid; b < B; b += nt) {
-            const uint32_t c = cursor[b] + lbase[b + 1];
-            cursor[b] = c;
-            if (gend) pref[(uint64_t(g) * nqs + ((j + 1) / spg)) * B + b] = uint16_t(min(c, pg.cap));
-        }
     }
     lds_barrier();
     for (uint32_t b = tid; b < B; b += nt) {
-        const uint32_t t = min(cursor[b], pg.cap);
+        const uint32_t t = min(cb[b] + lbase[b + 1], pg.cap);
         fill[uint64_t(b) * pg.G + g] = t;
         if constexpr (PROBE)  // the open last group and any the workgroup did not reach
             for (uint32_t q = (j + spg - 1) / spg; q <= pg.nq; ++q) pref[(uint64_t(g) * nqs + q) * B + b] = uint16_t(t);

@@ -3,7 +3,7 @@
 # abort / timeout (exit codes other than 0 and 1).  Usage: tools/gpu_session.sh STEP...
 #   smoke pytest bench benchq prof profq traffic pmcall others bench_c1 bench_c3 bench_c4
 #   bench_c5 bench_c5mixed bench_sst prof_c3 prof_c4 prof_c5 traffic_c3 pmc_c3 ab ab_c3 ab_c4
-#   ab_c5 selflaunch final
+#   ab_c5 abenv abenv_c5 selflaunch final
 # A/B steps run the default library and every build/variants/*.so (PBF_LIB), alternating, with
 # PBF_AB_ARGS appended to the bench command line.
 set -u
@@ -30,6 +30,13 @@ traffic() {  # tag bench-args...: FETCH_SIZE and WRITE_SIZE in separate passes, 
   run pmc_fetch_$tag 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_fetch_$tag -o run -- python bench.py --no-cpu-baseline --no-host-inclusive "$@"
   run pmc_write_$tag 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_write_$tag -o run -- python bench.py --no-cpu-baseline --no-host-inclusive "$@"
   python tools/traffic_summary.py gpurun_out/pmc_fetch_$tag gpurun_out/pmc_write_$tag gpurun_out/traffic_$tag.json --config $tag > gpurun_out/traffic_${tag}_summary.txt 2>&1 || true
+}
+abenv() {  # tag seconds rounds bench-args...: the default vs the environment in PBF_AB_ENV (VAR=value)
+  local tag=$1 secs=$2 rounds=$3; shift 3
+  for r in $(seq 1 $rounds); do
+    run ${tag}_default_$r $secs python bench.py --no-cpu-baseline --no-host-inclusive "$@"
+    run ${tag}_env_$r $secs env $PBF_AB_ENV python bench.py --no-cpu-baseline --no-host-inclusive "$@"
+  done
 }
 ab() {  # tag seconds rounds bench-args...
   local tag=$1 secs=$2 rounds=$3; shift 3
@@ -75,6 +82,8 @@ for step in "$@"; do
                   nm=$(basename $v .so)
                   PBF_LIB=$PWD/$v run parity_$nm 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_multi.py tests/test_gpu_lsm_get.py tests/test_gpu_device_resident.py -m gpu -x -q -rf --timeout 150 --timeout-method thread -k "${PBF_PARITY_K:-not config4 and not config3}"
                 done ;;
+    abenv) abenv abenv 300 2 --steps 50 --warmup 5 ;;
+    abenv_c5) abenv abenvc5 300 1 --config c5 --steps 5 --warmup 2 --no-host-c5 ;;
     ab_c3) ab abc3 300 1 --config c3 --steps 3 --warmup 1 ;;
     ab_c4) ab abc4 400 1 --config c4 --steps 3 --warmup 1 ;;
     ab_c5) ab abc5 300 1 --config c5 --steps 5 --warmup 2 --no-host-c5 ;;
