@@ -3,7 +3,7 @@
 # abort / timeout (exit codes other than 0 and 1).  Usage: tools/gpu_session.sh STEP...
 #   smoke pytest bench benchq prof profq traffic pmcall others bench_c1 bench_c3 bench_c4
 #   bench_c5 bench_c5mixed bench_sst prof_c3 prof_c4 prof_c5 traffic_c3 pmc_c3 ab ab_c3 ab_c4
-#   ab_c5 abenv abenv_c5 selflaunch final
+#   ab_c5 ab_c5mixed abenv abenv_c5 selflaunch final
 # A/B steps run the default library and every build/variants/*.so (PBF_LIB), alternating, with
 # PBF_AB_ARGS appended to the bench command line.
 set -u
@@ -86,6 +86,7 @@ for step in "$@"; do
     abenv_c5) abenv abenvc5 300 1 --config c5 --steps 5 --warmup 2 --no-host-c5 ;;
     ab_c3) ab abc3 300 1 --config c3 --steps 3 --warmup 1 ;;
     ab_c4) ab abc4 400 1 --config c4 --steps 3 --warmup 1 ;;
+    ab_c5mixed) ab abc5m 300 1 --config c5mixed --steps 5 --warmup 2 ;;
     ab_c5) ab abc5 300 1 --config c5 --steps 5 --warmup 2 --no-host-c5 ;;
     selflaunch) export PBF_BENCH_DEVICE=0 PBF_BENCH_BACKEND=gloo
                 run sl_c2_n2 300 python bench.py --gpus 2 --steps 10 --warmup 3 --no-host-inclusive
