@@ -311,7 +311,7 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
 //   so a failed quad starts from its group instead of a binary search over the row.
 // NFM: compile-time bound on nf (1 for a single filter: no per-filter registers or loops).
 template <int NFM>
-__global__ void __launch_bounds__(512) k_gather_ring(TileMap tm, PartGeom pg, uint64_t n,
+__device__ __forceinline__ void gather_ring_body(TileMap tm, PartGeom pg, uint64_t n,
                                                      const uint32_t* __restrict__ regions,
                                                      const uint32_t* __restrict__ R, const uint32_t* __restrict__ fill,
                                                      const uint16_t* __restrict__ pref,
@@ -502,6 +502,27 @@ __global__ void __launch_bounds__(512) k_gather_ring(TileMap tm, PartGeom pg, ui
         else
             for (uint64_t q = 0; q < nbt; ++q) hitmask[key0 / 8 + q] = uint8_t(bits >> (8 * q));
     }
+}
+
+// One filter: capped at 64 VGPRs so 8 waves per SIMD (4 workgroups per CU, the LDS limit) stay
+// resident; the set gather keeps its registers (one LDS key bitmap and result word per filter).
+template <int NFM>
+__global__ void __launch_bounds__(512) k_gather_ring(TileMap tm, PartGeom pg, uint64_t n,
+                                                     const uint32_t* __restrict__ regions,
+                                                     const uint32_t* __restrict__ R, const uint32_t* __restrict__ fill,
+                                                     const uint16_t* __restrict__ pref,
+                                                     const uint32_t* __restrict__ neg, uint8_t* __restrict__ hitmask,
+                                                     uint32_t* __restrict__ hw, uint32_t nf, uint64_t r_stride,
+                                                     uint64_t neg_stride, uint32_t tq) {
+    gather_ring_body<NFM>(tm, pg, n, regions, R, fill, pref, neg, hitmask, hw, nf, r_stride, neg_stride, tq);
+}
+template <>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(8)))
+k_gather_ring<1>(TileMap tm, PartGeom pg, uint64_t n, const uint32_t* __restrict__ regions,
+                 const uint32_t* __restrict__ R, const uint32_t* __restrict__ fill, const uint16_t* __restrict__ pref,
+                 const uint32_t* __restrict__ neg, uint8_t* __restrict__ hitmask, uint32_t* __restrict__ hw, uint32_t nf,
+                 uint64_t r_stride, uint64_t neg_stride, uint32_t tq) {
+    gather_ring_body<1>(tm, pg, n, regions, R, fill, pref, neg, hitmask, hw, nf, r_stride, neg_stride, tq);
 }
 
 }  // namespace pbf
