@@ -217,7 +217,9 @@ int pbf_key_range_mask(int device, void* stream, const uint8_t* keys, const uint
 
 /* Synthetic keys straight into device memory (bench / tests; definitions in
  * pebbledb_amd/keys.py): 16 hex chars of splitmix64(seed + start + i), and the variable-length
- * 8..64-byte family (offsets must already hold the n+1 offsets, relative to offsets[0]). */
+ * 8..64-byte family (offsets must already hold the n+1 offsets, relative to offsets[0]).
+ * stream = NULL: the keys are complete on return (filters run on non-blocking streams, which the
+ * null stream does not order); otherwise asynchronous on `stream`. */
 int pbf_gen_splitmix_hex(int device, void* stream, uint8_t* out_dev, uint64_t seed, uint64_t start, uint64_t n);
 int pbf_gen_varlen(int device, void* stream, uint8_t* out_dev, const uint64_t* offsets_dev, uint64_t seed,
                    uint64_t start, uint64_t n);

@@ -855,13 +855,14 @@ int run_tiled_probe_set(pbf_filter_t* f, pbf_filter_t* const* fs, uint32_t nf, c
     for (uint32_t i = 0; i < nf; ++i) ps.bm[i] = fs[i]->bitmap;
     size_t lds_tile = ((size_t(1) << tm.tb) / 32 + 2 * pg.G + 1 + 16) * 4;
     // the tile test's per-word table: u32 global word index + u8 filled-entry count per word
-    const size_t lds_expand = size_t(pg.G) * (pg.cap / 32) * 5;
-    const bool expand = lds_tile + lds_expand <= 160 * 1024;
-    if (expand) lds_tile += lds_expand;
+    // (TAB 2, else the u16 region of every word: TAB 1, else a binary search: TAB 0)
+    const size_t table_words = size_t(pg.G) * (pg.cap / 32);
+    const int tab = lds_tile + table_words * 5 <= 160 * 1024 ? 2 : (lds_tile + table_words * 2 <= 160 * 1024 ? 1 : 0);
+    lds_tile += tab == 2 ? table_words * 5 : (tab == 1 ? table_words * 2 : 0);
     // a region word's global index (region * cap/32 + word) is 32-bit
     if (uint64_t(pg.G) * B * (pg.cap / 32) >= (uint64_t(1) << 32)) return fail(PBF_ERR_INVALID, "probe scratch too large");
-    auto tprobe = expand ? k_tile_probe<true> : k_tile_probe<false>;
-    auto tprobe_set = expand ? k_tile_probe_set<true> : k_tile_probe_set<false>;
+    auto tprobe = tab == 2 ? k_tile_probe<2> : (tab == 1 ? k_tile_probe<1> : k_tile_probe<0>);
+    auto tprobe_set = tab == 2 ? k_tile_probe_set<2> : (tab == 1 ? k_tile_probe_set<1> : k_tile_probe_set<0>);
     HIP_TRY(allow_lds(tprobe, lds_tile));
     // the partition zeroes neg (and presets hw for the gather) itself
     hipError_t err = hipSuccess;
@@ -2300,6 +2301,9 @@ int pbf_gen_splitmix_hex(int device, void* stream, uint8_t* out_dev, uint64_t se
     if (!out_dev || (reinterpret_cast<uintptr_t>(out_dev) & 15)) return fail(PBF_ERR_INVALID, "out must be 16-B aligned");
     k_gen_splitmix_hex<<<grid_for(n, 256), 256, 0, static_cast<hipStream_t>(stream)>>>(out_dev, seed, start, n);
     CHECK_LAUNCH();
+    // the null stream does not order the filters' non-blocking streams: with no stream given the
+    // keys are complete on return (a build enqueued next must not read them half-written)
+    if (!stream) HIP_TRY(hipStreamSynchronize(nullptr));
     return PBF_OK;
 }
 
@@ -2310,6 +2314,7 @@ int pbf_gen_varlen(int device, void* stream, uint8_t* out_dev, const uint64_t* o
     if (!out_dev || !offsets_dev) return fail(PBF_ERR_INVALID, "null pointer");
     k_gen_varlen<<<grid_for(n, 256), 256, 0, static_cast<hipStream_t>(stream)>>>(out_dev, offsets_dev, seed, start, n);
     CHECK_LAUNCH();
+    if (!stream) HIP_TRY(hipStreamSynchronize(nullptr));  // as pbf_gen_splitmix_hex
     return PBF_OK;
 }
 

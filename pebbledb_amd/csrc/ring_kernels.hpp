@@ -367,10 +367,11 @@ __device__ __forceinline__ void gather_ring_body(TileMap tm, PartGeom pg, uint64
     lds_barrier();
     constexpr int U = kGatherRegionsInFlight;
     for (uint32_t b0 = b_lo + wave; b0 < b_hi; b0 += nwaves * U) {
+        // a region's fill is its last group-boundary count (pref[nq]), already in LDS
         uint32_t fillb[U];
 #pragma unroll
         for (int u = 0; u < U; ++u)
-            fillb[u] = b0 + u * nwaves < b_hi ? fill[uint64_t(b0 + u * nwaves) * pg.G + g] : 0u;
+            fillb[u] = b0 + u * nwaves < b_hi ? uint32_t(lpref[(b0 + u * nwaves - b_lo) * nqs + pg.nq]) : 0u;
         uint32_t maxf = 0;
 #pragma unroll
         for (int u = 0; u < U; ++u) maxf = max(maxf, fillb[u]);
@@ -379,7 +380,8 @@ __device__ __forceinline__ void gather_ring_body(TileMap tm, PartGeom pg, uint64
             uint32_t rw[NFM][U];
             // single filter: result words first; a quad's entries (only their key ids are
             // needed) are loaded only when one of its entries failed, so quads that passed (a
-            // probe batch's members) cost their result bits alone (C2 probe 0.517 -> 0.504 ms).
+            // probe batch's members) cost their result bits alone (C2 probe 0.517 -> 0.504 ms;
+            // re-measured against loading both together: 0.482 vs 0.520 ms, profiles/r03/s11).
             // Multi-filter sets: nearly every quad fails some filter, so entries and result
             // words go out together.
             uint32_t anyq[U];  // one filter: the quad's failed entries as byte-spread bits (0: skip)

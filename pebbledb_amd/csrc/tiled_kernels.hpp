@@ -541,12 +541,14 @@ __global__ void __launch_bounds__(256) k_ovf_build(TileMap tm, const uint32_t* _
 // piece of a word, so an instruction reads 1 KiB contiguously (words are consecutive within a
 // region).  Each lane tests its 4 entries in the LDS tile; four ballots give every word's 32
 // result bits, stored by the word's first lane.
-// EXPAND (the LDS budget allows it): a per-word table gives word c's global index
+// TAB = 2 (the LDS budget allows it): a per-word table gives word c's global index
 // wo = region * (cap / 32) + word-in-region — the region word's address / 32 AND its result
 // word's index — and its count of filled entries, so a load needs one LDS read and the wave's
-// U loads issue back to back.  Otherwise the word's region comes from a binary search over the
-// word prefix.
-template <bool NT, bool EXPAND>
+// U loads issue back to back.  TAB = 1 (5 B per word do not fit, 2 B do: C3's 4096 tiles with
+// ~1000-entry regions): a u16 table gives the word's region, its word-in-region and fill come
+// from the region's word prefix and fill (three LDS reads).  TAB = 0: the word's region comes from
+// a binary search over the word prefix.
+template <bool NT, int TAB>
 __device__ __forceinline__ void tile_probe_body(uint32_t* smem, uint32_t b, const TileMap& tm, const PartGeom& pg,
                                                 const uint32_t* __restrict__ regions, const uint32_t* __restrict__ fill,
                                                 const uint32_t* __restrict__ bitmap, uint32_t* __restrict__ R) {
@@ -556,8 +558,9 @@ __device__ __forceinline__ void tile_probe_body(uint32_t* smem, uint32_t b, cons
     uint32_t* fills = tile + W;     // G
     uint32_t* wpre = fills + G;     // G+1
     uint32_t* ws = wpre + G + 1;    // 16
-    uint32_t* wo = ws + 16;                                     // G*wpr (EXPAND)
-    uint8_t* wn = reinterpret_cast<uint8_t*>(wo + G * wpr);     // G*wpr (EXPAND)
+    uint32_t* wo = ws + 16;                                     // G*wpr (TAB 2)
+    uint8_t* wn = reinterpret_cast<uint8_t*>(wo + G * wpr);     // G*wpr (TAB 2)
+    uint16_t* wq = reinterpret_cast<uint16_t*>(ws + 16);        // G*wpr (TAB 1)
     const uint64_t w0 = tile_word0(b, tm);
     const uint32_t nw = uint32_t(min<uint64_t>(W, tm.total_words - w0));
     const uint32_t tid = threadIdx.x, nt = blockDim.x;
@@ -568,13 +571,15 @@ __device__ __forceinline__ void tile_probe_body(uint32_t* smem, uint32_t b, cons
     for (uint32_t q = tid; q < G; q += nt) {
         const uint32_t fq = fill[uint64_t(b) * G + q];
         fills[q] = fq;  // entries again
-        if constexpr (EXPAND) {
+        if constexpr (TAB == 2) {
             const uint32_t base = uint32_t(region_id(q, b, G, B)) * wpr;
             for (uint32_t c = wpre[q]; c < wpre[q + 1]; ++c) {
                 const uint32_t word = c - wpre[q];
                 wo[c] = base + word;
                 wn[c] = uint8_t(min(fq - word * 32, 32u));
             }
+        } else if constexpr (TAB == 1) {
+            for (uint32_t c = wpre[q]; c < wpre[q + 1]; ++c) wq[c] = uint16_t(q);
         }
     }
     lds_barrier();
@@ -590,11 +595,11 @@ __device__ __forceinline__ void tile_probe_body(uint32_t* smem, uint32_t b, cons
         for (int u = 0; u < U; ++u) {
             const uint32_t c = c0 + u * stride + wsub;
             const uint32_t cc = min(c, total - 1);  // unconditional loads
-            if constexpr (EXPAND) {
+            if constexpr (TAB == 2) {
                 oo[u] = wo[cc];
                 lim[u] = c < total ? uint32_t(wn[cc]) : 0u;  // entries past the fill read as 0
             } else {
-                const uint32_t qq = bucket_of(wpre, G, cc);
+                const uint32_t qq = TAB == 1 ? uint32_t(wq[cc]) : bucket_of(wpre, G, cc);
                 const uint32_t word = cc - wpre[qq];
                 oo[u] = uint32_t(region_id(qq, b, G, B)) * wpr + word;
                 lim[u] = c < total ? min(fills[qq] - word * 32, 32u) : 0u;
@@ -625,12 +630,12 @@ __device__ __forceinline__ void tile_probe_body(uint32_t* smem, uint32_t b, cons
     }
 }
 
-template <bool EXPAND>
+template <int TAB>
 __global__ void __launch_bounds__(1024) k_tile_probe(TileMap tm, PartGeom pg, const uint32_t* __restrict__ regions,
                                                      const uint32_t* __restrict__ fill,
                                                      const uint32_t* __restrict__ bitmap, uint32_t* __restrict__ R) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-    tile_probe_body<kNtLoad, EXPAND>(smem, blockIdx.x, tm, pg, regions, fill, bitmap, R);
+    tile_probe_body<kNtLoad, TAB>(smem, blockIdx.x, tm, pg, regions, fill, bitmap, R);
 }
 
 // The tile test of a multi-filter probe in ONE launch: workgroup (tile b, filter f) for every
@@ -638,7 +643,7 @@ __global__ void __launch_bounds__(1024) k_tile_probe(TileMap tm, PartGeom pg, co
 // only, never correctness), so block x = ((b / 8) * nf + f) * 8 + b % 8 puts the nf
 // workgroups of tile b on one XCD, dispatched together: they stream the same region entries
 // (g, b), g = 0..G-1, in the same order, and all but the first read them from that XCD's L2.
-template <bool EXPAND>
+template <int TAB>
 __global__ void __launch_bounds__(1024) k_tile_probe_set(TileMap tm, PartGeom pg, const uint32_t* __restrict__ regions,
                                                          const uint32_t* __restrict__ fill, ProbeSet ps,
                                                          uint32_t* __restrict__ R, uint64_t r_stride) {
@@ -649,7 +654,7 @@ __global__ void __launch_bounds__(1024) k_tile_probe_set(TileMap tm, PartGeom pg
     const uint32_t b = (t / nf) * 8 + (x & 7);
     if (b >= tm.nbuckets) return;
     // the set's other workgroups of tile b read the same lines: temporal loads keep them in L2
-    tile_probe_body<false, EXPAND>(smem, b, tm, pg, regions, fill, ps.bm[f], R + f * r_stride);
+    tile_probe_body<false, TAB>(smem, b, tm, pg, regions, fill, ps.bm[f], R + f * r_stride);
 }
 
 // hw (ANDed gather words, one per 32 keys) → the LSB-first hit mask of n keys.

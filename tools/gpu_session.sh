@@ -2,7 +2,7 @@
 # One GPU-box session: each GPU step under its own time limit; stop at the first fault /
 # abort / timeout (exit codes other than 0 and 1).  Usage: tools/gpu_session.sh STEP...
 #   smoke pytest bench benchq prof profq traffic pmcall others bench_c1 bench_c3 bench_c4
-#   bench_c5 bench_c5mixed bench_sst prof_c3 prof_c4 prof_c5 traffic_c3 pmc_c3 ab ab_c3 ab_c4
+#   bench_c5 bench_c5mixed bench_sst prof_c3 prof_c4 prof_c5 traffic_c3 pmc_c3 pmc_c4 ab ab_c3 ab_c4
 #   ab_c5 ab_c5mixed abenv abenv_c5 selflaunch final
 # A/B steps run the default library and every build/variants/*.so (PBF_LIB), alternating, with
 # PBF_AB_ARGS appended to the bench command line.
@@ -62,6 +62,7 @@ for step in "$@"; do
     traffic_c3) traffic c3 --config c3 --steps 2 --warmup 1 ;;
     pmcall) run pmcall 2400 tools/pmc_passes.sh gpurun_out/pmcall ;;
     pmc_c3) run pmc_c3 2400 tools/pmc_passes.sh gpurun_out/pmc_c3 --config c3 ;;
+    pmc_c4) run pmc_c4 2400 tools/pmc_passes.sh gpurun_out/pmc_c4 --config c4 ;;
     bench_c1) run bench_c1 300 python bench.py --config c1 --steps 50 --warmup 5 ;;
     bench_c3) run bench_c3 600 python bench.py --config c3 --steps 5 --warmup 2 ;;
     bench_c4) run bench_c4 600 python bench.py --config c4 --steps 3 --warmup 1 ;;
