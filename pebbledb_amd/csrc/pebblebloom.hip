@@ -613,7 +613,12 @@ void set_gather(PartPlan& pl, uint32_t B, uint32_t row, uint32_t nf = 1) {
     const size_t kb = size_t((pl.pg.kpw + 31) / 32) * 4 * nf;  // one key bitmap per fused filter
     uint32_t S = gather_splits();
     auto lds = [&](uint32_t sp) { return kb + size_t((B + sp - 1) / sp) * row * 2 + 16; };
+    auto per_cu = [](size_t bytes) { return std::min<size_t>(4, (160 * 1024) / bytes); };  // 512-thread WGs
     while (lds(S) > 156 * 1024 && S < 64 && S < B) S *= 2;
+    // more splits while they raise the workgroups per CU (the gather waits on memory; each split
+    // ANDs its key words into hw once): C3 (4096 tiles, 65 boundary counts per tile) 8 -> 32
+    // splits, probe 14.42 -> 13.40 ms; C2 / C5 keep 8 (profiles/r03/s12)
+    while (S < 32 && S < B && per_cu(lds(2 * S)) > per_cu(lds(S))) S *= 2;
     pl.gsplit = S;
     pl.lds_gather = lds(S);
     pl.gtq = 0;
