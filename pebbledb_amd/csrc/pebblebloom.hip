@@ -908,7 +908,9 @@ int run_tiled_probe_set(pbf_filter_t* f, pbf_filter_t* const* fs, uint32_t nf, c
         tprobe_set<<<tgrid, 1024, lds_tile, s>>>(tm, pg, regions, fill, ps, R, r_words);
     }
     LAUNCHED(f, nf == 1 ? "k_tile_probe" : "k_tile_probe_set");
-    gather<<<grid, 512, pl.lds_gather, s>>>(tm, pg, b.n, regions, R, fill, pref, neg, hitmasks[0] + hm_off, hw, nf,
+    // the set gather: 1024 threads when its LDS admits one workgroup per CU (C5's 8 key bitmaps)
+    const uint32_t gthreads = nf > 1 && pl.lds_gather > 80 * 1024 ? 1024 : 512;
+    gather<<<grid, gthreads, pl.lds_gather, s>>>(tm, pg, b.n, regions, R, fill, pref, neg, hitmasks[0] + hm_off, hw, nf,
                                            r_words, neg_words, pl.gtq);
     LAUNCHED(f, "k_gather_ring");
     if (use_hw) {

@@ -506,10 +506,12 @@ __device__ __forceinline__ void gather_ring_body(TileMap tm, PartGeom pg, uint64
     }
 }
 
-// One filter: capped at 64 VGPRs so 8 waves per SIMD (4 workgroups per CU, the LDS limit) stay
-// resident; the set gather keeps its registers (one LDS key bitmap and result word per filter).
+// One filter: 512 threads, capped at 64 VGPRs so 8 waves per SIMD (4 workgroups per CU, the LDS
+// limit) stay resident.  The set gather keeps its registers (one LDS key bitmap and result word
+// per filter) and, as its LDS admits one workgroup per CU, runs 1024 threads (16 waves) when
+// the host launches it so.
 template <int NFM>
-__global__ void __launch_bounds__(512) k_gather_ring(TileMap tm, PartGeom pg, uint64_t n,
+__global__ void __launch_bounds__(1024) k_gather_ring(TileMap tm, PartGeom pg, uint64_t n,
                                                      const uint32_t* __restrict__ regions,
                                                      const uint32_t* __restrict__ R, const uint32_t* __restrict__ fill,
                                                      const uint16_t* __restrict__ pref,
