@@ -1,6 +1,6 @@
 """HBM traffic per pass from rocprofv3 PMC passes (tools/gpu_session.sh step `traffic`).
 
-    python tools/traffic_summary.py FETCH_DIR WRITE_DIR OUT.json [--config c2]
+    python tools/traffic_summary.py FETCH_DIR WRITE_DIR OUT.json [--config c2] [--probe-scale X]
 
 FETCH_SIZE and WRITE_SIZE come from separate `--pmc` runs of the same short bench (one counter
 group per run: FETCH_SIZE uses 3 of the 4 TCC slots, WRITE_SIZE 2).  Both are in KiB.  Per
@@ -10,7 +10,10 @@ MI355X_MICROARCH.md §HBM, on gfx950 FETCH_SIZE reports exactly half the bytes o
 (keys, region entries); the random word reads of the probe's spill path are negligible.
 
 Per kernel the median over dispatches of the full-size launches is taken; a pass's traffic is
-the sum over its kernels.  bench.py reads OUT.json to fill `roofline.traffic`.
+the sum over its kernels.  A pass split into several pipelines (C3's probe: 200M keys in
+pipelines of at most 2^30 positions, 134.2M keys at k = 8) is scaled from its full-size launch
+by keys (--probe-scale = keys per pass / keys per full-size launch).  bench.py reads OUT.json to
+fill `roofline.traffic`.
 """
 from __future__ import annotations
 
@@ -58,6 +61,7 @@ def pass_of(kernel: str) -> str | None:
 def main() -> None:
     fdir, wdir, out = sys.argv[1:4]
     config = sys.argv[sys.argv.index("--config") + 1] if "--config" in sys.argv else "c2"
+    pscale = float(sys.argv[sys.argv.index("--probe-scale") + 1]) if "--probe-scale" in sys.argv else 1.0
     fetch = per_kernel(fdir, "FETCH_SIZE")
     write = per_kernel(wdir, "WRITE_SIZE")
     res = {"config": config, "source": f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE ({fdir}, {wdir})",
@@ -73,6 +77,10 @@ def main() -> None:
         agg = res["passes"].setdefault(p, {"read_bytes": 0.0, "write_bytes": 0.0})
         agg["read_bytes"] += rd
         agg["write_bytes"] += wr
+    if pscale != 1.0 and "probe" in res["passes"]:
+        res["probe_scale"] = pscale
+        for key in ("read_bytes", "write_bytes"):
+            res["passes"]["probe"][key] *= pscale
     for p in res["passes"].values():
         p["traffic_bytes"] = p["read_bytes"] + p["write_bytes"]
     # the kernels these counters were taken on (bench.py only uses a summary of its own sources)
