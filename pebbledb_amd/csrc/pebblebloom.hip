@@ -913,12 +913,12 @@ int run_tiled_probe_set(pbf_filter_t* f, pbf_filter_t* const* fs, uint32_t nf, c
     gather<<<grid, gthreads, pl.lds_gather, s>>>(tm, pg, b.n, regions, R, fill, pref, neg, hitmasks[0] + hm_off, hw, nf,
                                            r_words, neg_words, pl.gtq);
     LAUNCHED(f, "k_gather_ring");
-    if (use_hw) {
-        for (uint32_t i = 0; i < nf; ++i) {
-            k_hw_to_hitmask<<<grid_for(neg_words, 256, 4096), 256, 0, s>>>(hw + i * neg_words, b.n,
-                                                                           hitmasks[i] + hm_off);
-            LAUNCHED(f, "k_hw_to_hitmask");
-        }
+    if (use_hw) {  // every filter's hit mask in one launch
+        HitMasks hms{};
+        for (uint32_t i = 0; i < nf; ++i) hms.hm[i] = hitmasks[i] + hm_off;
+        const dim3 hgrid(std::max<uint32_t>(1, grid_for(neg_words, 256, 4096) / nf), nf);
+        k_hw_to_hitmask<<<hgrid, 256, 0, s>>>(hw, neg_words, b.n, hms);
+        LAUNCHED(f, "k_hw_to_hitmask");
     }
     return PBF_OK;
 }

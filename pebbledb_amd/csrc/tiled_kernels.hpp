@@ -657,12 +657,18 @@ __global__ void __launch_bounds__(1024) k_tile_probe_set(TileMap tm, PartGeom pg
     tile_probe_body<false, TAB>(smem, b, tm, pg, regions, fill, ps.bm[f], R + f * r_stride);
 }
 
-// hw (ANDed gather words, one per 32 keys) → the LSB-first hit mask of n keys.
-__global__ void k_hw_to_hitmask(const uint32_t* __restrict__ hw, uint64_t n, uint8_t* __restrict__ hitmask) {
+// hw (ANDed gather words, one per 32 keys) → the LSB-first hit masks of n keys, for every filter
+// of a set in one launch (grid y = filter; filter f's words at hw + f * stride).
+struct HitMasks {
+    uint8_t* hm[kMaxProbeSet];
+};
+__global__ void k_hw_to_hitmask(const uint32_t* __restrict__ hw, uint64_t stride, uint64_t n, HitMasks out) {
     const uint64_t nw = (n + 31) / 32;
+    const uint32_t* src = hw + uint64_t(blockIdx.y) * stride;
+    uint8_t* hitmask = out.hm[blockIdx.y];
     for (uint64_t w = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; w < nw; w += uint64_t(gridDim.x) * blockDim.x) {
         const uint64_t key0 = w * 32;
-        const uint32_t bits = hw[w];
+        const uint32_t bits = src[w];
         const uint64_t nbt = min<uint64_t>(4, (n - key0 + 7) / 8);
         if (nbt == 4 && (reinterpret_cast<uintptr_t>(hitmask + key0 / 8) & 3) == 0)
             *reinterpret_cast<uint32_t*>(hitmask + key0 / 8) = bits;
