@@ -685,7 +685,9 @@ PartPlan plan_partition(uint32_t B, uint32_t k, int km, uint64_t n, bool probe, 
     pl.pg.nq = uint32_t((kpw + kGroupKeys - 1) / kGroupKeys);
     const double mu = double(kpw) * k * share;
     const uint64_t cap = uint64_t(mu + 8.0 * std::sqrt(mu) + 32.0);
-    pl.pg.cap = uint32_t(((cap + 31) / 32) * 32);
+    // (k_part addresses an entry by a 24-bit multiply-add within its workgroup's regions)
+    pl.pg.cap = uint32_t(std::min<uint64_t>(((cap + 31) / 32) * 32, ((uint64_t(1) << 32) - 1) / std::max<uint32_t>(B, 1) & ~uint64_t(31)));
+    pl.pg.cap = std::min<uint32_t>(pl.pg.cap, (1u << 24) - 32);
     set_gather(pl, B, pl.pg.nq + 1, nf);
     return pl;
 }

@@ -240,6 +240,7 @@ __global__ void __launch_bounds__(kPartThreads) k_part(KeySet ks, uint64_t n, in
     uint32_t* stage = ws + 16;         // kps * k
     uint16_t* bkt = reinterpret_cast<uint16_t*>(stage + pg.kps * uint32_t(k));  // kps * k (probes)
     const uint32_t lmask = (1u << tm.tb) - 1u;
+    uint32_t* const rgn = regions + uint64_t(g) * B * pg.cap;  // this workgroup's regions
     // probes: sub-chunks per 4096-key group (kps is 1024, 2048 or 4096 for probes) and the
     // group-boundary counts pref[g][q][b] (q = 0..nq, b fastest), as the ring partition keeps them
     const uint32_t spg = kGroupKeys / pg.kps, nqs = pg.nq + 1;
@@ -387,12 +388,16 @@ __global__ void __launch_bounds__(kPartThreads) k_part(KeySet ks, uint64_t n, in
             if (s1 + pg.kps < k1) load_keys(s1 + pg.kps);
         }
         // Lane-parallel write-out: entry e of the sorted stage goes to position cb[b] + e of
-        // region (g, b).  Eight entries per thread per batch, loads unconditional, so each thread
-        // has eight independent LDS → store chains in flight.  Positions >= cap overflow.
+        // region (g, b).  UW entries per thread per batch: the stage reads, then the cursor
+        // reads, are issued before any is consumed (one LDS wait each), and the
+        // region offsets are 32-bit within the workgroup's regions (B * cap < 2^32; b < 4096,
+        // cap < 2^24: one 24-bit multiply-add).  Positions >= cap overflow (rare).
         const uint32_t tot = lbase[B];
-        constexpr int UW = 8;
+        // (four per batch when the next sub-chunk's KPT x KMAX positions and ranks already hold
+        // 60 registers: C4's k = 10 build, which spills at eight)
+        constexpr int UW = KPT * KMAX >= 30 ? 4 : 8;
         for (uint32_t e0 = tid; e0 < tot; e0 += nt * UW) {
-            uint32_t v[UW], b[UW];
+            uint32_t v[UW], b[UW], r[UW];
 #pragma unroll
             for (int u = 0; u < UW; ++u) {
                 const uint32_t e = min(e0 + u * nt, tot - 1);
@@ -400,17 +405,23 @@ __global__ void __launch_bounds__(kPartThreads) k_part(KeySet ks, uint64_t n, in
                 b[u] = PROBE ? uint32_t(bkt[e]) : (v[u] >> tm.tb);
             }
 #pragma unroll
+            for (int u = 0; u < UW; ++u) r[u] = cb[b[u]] + e0 + u * nt;
+            uint32_t over = 0;
+#pragma unroll
             for (int u = 0; u < UW; ++u) {
-                const uint32_t e = e0 + u * nt;
-                const uint32_t r = cb[b[u]] + e;
-                if (e < tot) {
-                    if (r < pg.cap) {
-                        regions[region_id(g, b[u], pg.G, B) * pg.cap + r] = v[u];
-                    } else if constexpr (PROBE) {
-                        spill_probe(ps, pos_to_bit((b[u] << tm.tb) | (v[u] & lmask), tm),
-                                    s0 + ((v[u] >> kSlotShift) & (pg.kps - 1)));
-                    } else {
-                        ovf[atomicAdd(ovf_count, 1u)] = v[u];
+                const bool live = e0 + u * nt < tot;
+                if (live && r[u] < pg.cap) rgn[__umul24(b[u], pg.cap) + r[u]] = v[u];
+                over |= uint32_t(live && r[u] >= pg.cap) << u;
+            }
+            if (over) {  // region overflow: heavy key duplication only
+#pragma unroll
+                for (int u = 0; u < UW; ++u) {
+                    if ((over >> u) & 1u) {
+                        if constexpr (PROBE)
+                            spill_probe(ps, pos_to_bit((b[u] << tm.tb) | (v[u] & lmask), tm),
+                                        s0 + ((v[u] >> kSlotShift) & (pg.kps - 1)));
+                        else
+                            ovf[atomicAdd(ovf_count, 1u)] = v[u];
                     }
                 }
             }
