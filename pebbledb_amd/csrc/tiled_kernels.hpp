@@ -363,7 +363,19 @@ __global__ void __launch_bounds__(kPartThreads) k_part(KeySet ks, uint64_t n, in
         scan_advance(PROBE && j > 0 && (j & (spg - 1)) == 0, j / spg);
         // place the sub-chunk's entries, sorted by tile, into the stage (the key's place in its
         // 4096-key group goes into a probe entry); cnt is free again
+        // Every tile base is read before the first stage write: interleaved, each write's
+        // address waited on its own LDS read (the compiler cannot tell stage from lbase).  (Not
+        // for the k > 16 register buckets, which would spill.)
+        constexpr bool HOIST = KPT * KMAX < 32;
         const uint32_t gkey0 = (j & (spg - 1)) * pg.kps;
+        if constexpr (HOIST) {
+#pragma unroll
+            for (int u = 0; u < KPT; ++u) {
+#pragma unroll
+                for (int s = 0; s < KMAX; ++s)
+                    if (s < k) rk[u * KMAX + s] += lbase[pos[u * KMAX + s] >> tm.tb];  // the entry's slot
+            }
+        }
 #pragma unroll
         for (int u = 0; u < KPT; ++u) {
             const uint32_t slot_key = u * nt + tid;
@@ -372,7 +384,7 @@ __global__ void __launch_bounds__(kPartThreads) k_part(KeySet ks, uint64_t n, in
                 for (int s = 0; s < KMAX; ++s) {
                     if (s < k) {
                         const uint32_t p = pos[u * KMAX + s];
-                        const uint32_t slot = lbase[p >> tm.tb] + rk[u * KMAX + s];
+                        const uint32_t slot = HOIST ? rk[u * KMAX + s] : lbase[p >> tm.tb] + rk[u * KMAX + s];
                         stage[slot] = PROBE ? (((gkey0 + slot_key) << kSlotShift) | (p & lmask)) : p;
                         if constexpr (PROBE) bkt[slot] = uint16_t(p >> tm.tb);
                     }
