@@ -961,14 +961,33 @@ bool want_tiled_probe(pbf_filter_t* f, uint64_t n) {
 // Largest probe batch one tiled pipeline takes: the gather keeps a u16 run-boundary table
 // (B x (nq+1), one row per 4096-key group) and a bit per key of its workgroup in LDS, and
 // positions stay u32.
-uint64_t tiled_probe_batch(pbf_filter_t* f, int km, uint32_t nf = 1) {
+// Keys per tiled-probe pipeline for a batch of `total` keys: the largest batch whose gather
+// workgroup fits the LDS (halving, then a search between the last two sizes in 64Ki-key steps),
+// then the batch split into equal pipelines (C5's 100M keys: 3 x 33.3M instead of 4 x 22.4M +
+// 10.4M — every pipeline streams the filters' bitmaps once, however few keys it holds).
+uint64_t tiled_probe_batch(pbf_filter_t* f, int km, uint32_t nf, uint64_t total) {
     const uint32_t k = f->k;
-    uint64_t n = std::max<uint64_t>(64, (kMaxPositions / k) & ~uint64_t(63));
-    for (;;) {
-        const PartPlan pl = plan_for(f->tm, k, km, n, true, nf);
-        if ((pl.lds_gather <= 156 * 1024 && pl.pg.cap <= 65535) || n <= 64 * 1024) return n;
-        n = std::max<uint64_t>(64 * 1024, (n / 2) & ~uint64_t(63));
+    auto fits = [&](uint64_t m) {
+        const PartPlan pl = plan_for(f->tm, k, km, m, true, nf);
+        return pl.lds_gather <= 156 * 1024 && pl.pg.cap <= 65535;
+    };
+    const uint64_t top = std::max<uint64_t>(64, (kMaxPositions / k) & ~uint64_t(63));
+    uint64_t n = top;
+    while (n > 64 * 1024 && !fits(n)) n = std::max<uint64_t>(64 * 1024, (n / 2) & ~uint64_t(63));
+    if (n < top && n >= 64 * 1024) {
+        uint64_t lo = n, hi = std::min<uint64_t>(2 * n, top);
+        while (hi - lo > 65536) {
+            const uint64_t mid = ((lo + hi) / 2) & ~uint64_t(65535);
+            if (mid <= lo) break;
+            (fits(mid) ? lo : hi) = mid;
+        }
+        n = lo;
     }
+    if (total > n) {  // equal pipelines, each a multiple of 64 keys (whole hit-mask words)
+        const uint64_t np = (total + n - 1) / n;
+        n = std::min<uint64_t>(n, (((total + np - 1) / np) + 63) & ~uint64_t(63));
+    }
+    return n;
 }
 
 int add_device(pbf_filter_t* f, const Batch& b) {
@@ -992,7 +1011,7 @@ int probe_device(pbf_filter_t* f, const Batch& b, uint8_t* hitmask_dev) {
     int rc = materialise(f);
     if (rc) return rc;
     if (want_tiled_probe(f, b.n)) {
-        const uint64_t per = tiled_probe_batch(f, b.km);
+        const uint64_t per = tiled_probe_batch(f, b.km, 1, b.n);
         for (uint64_t i0 = 0; i0 < b.n; i0 += per) {
             rc = run_tiled_probe(f, slice(b, i0, std::min<uint64_t>(per, b.n - i0)), hitmask_dev + i0 / 8);
             if (rc) return rc;
@@ -1127,7 +1146,7 @@ int probe_multi_device(pbf_filter_t* const* fs, uint32_t nf, const Batch& b, uin
         }
     }
     if (shared_probe(fs, nf, b.n)) {
-        const uint64_t per = tiled_probe_batch(f0, b.km, std::min<uint32_t>(nf, kMaxProbeSet));
+        const uint64_t per = tiled_probe_batch(f0, b.km, std::min<uint32_t>(nf, kMaxProbeSet), b.n);
         for (uint64_t i0 = 0; i0 < b.n; i0 += per) {
             const Batch c = slice(b, i0, std::min<uint64_t>(per, b.n - i0));
             for (uint32_t g0 = 0; g0 < nf; g0 += kMaxProbeSet) {
