@@ -59,7 +59,7 @@ for step in "$@"; do
     prof) prof prof 600 --steps 20 --warmup 5 --no-cpu-baseline --no-host-inclusive ;;
     profq) prof profq 300 --steps 20 --warmup 5 --no-cpu-baseline --no-host-inclusive ;;
     traffic) traffic c2 --steps 5 --warmup 2 ;;
-    traffic_c3) traffic c3 --config c3 --steps 2 --warmup 1 ;;  # then re-run traffic_summary with --probe-scale 1.4901161
+    traffic_c3) traffic c3 --config c3 --steps 2 --warmup 1 ;;  # then re-run traffic_summary with --probe-scale 2.0 (two equal 100M-key pipelines)
     pmcall) run pmcall 2400 tools/pmc_passes.sh gpurun_out/pmcall ;;
     pmc_c3) run pmc_c3 2400 tools/pmc_passes.sh gpurun_out/pmc_c3 --config c3 ;;
     pmc_c4) run pmc_c4 2400 tools/pmc_passes.sh gpurun_out/pmc_c4 --config c4 ;;

@@ -10,9 +10,9 @@ MI355X_MICROARCH.md §HBM, on gfx950 FETCH_SIZE reports exactly half the bytes o
 (keys, region entries); the random word reads of the probe's spill path are negligible.
 
 Per kernel the median over dispatches of the full-size launches is taken; a pass's traffic is
-the sum over its kernels.  A pass split into several pipelines (C3's probe: 200M keys in
-pipelines of at most 2^30 positions, 134.2M keys at k = 8) is scaled from its full-size launch
-by keys (--probe-scale = keys per pass / keys per full-size launch).  bench.py reads OUT.json to
+the sum over its kernels.  A pass split into several pipelines (C3's probe: 200M keys in two
+equal pipelines of 100M, each under the 2^30-position limit) is scaled from its full-size launch
+by keys (--probe-scale = keys per pass / keys per full-size launch = 2.0 for C3).  bench.py reads OUT.json to
 fill `roofline.traffic`.
 """
 from __future__ import annotations
