@@ -224,6 +224,7 @@ def dropin_latency(device, reps=2000):
     out["identical"] = (out["pebbledb_amd"]["bitmap_sha16"] == out["reference_port"]["bitmap_sha16"]
                         and out["pebbledb_amd"]["hits"] == out["reference_port"]["hits"])
     out["get_16_filters"] = get_set_latency(device)
+    out["reader_threads"] = reader_threads(device)
     return out
 
 
@@ -256,6 +257,47 @@ def get_set_latency(device, reps=1000):
     return {"filters": len(flat), "nb_bytes": [bf.nb_bytes for bf in flat],
             "one_launch_us_per_get": round(t_set / reps * 1e6, 2),
             "may_contain_x16_us_per_get": round(t_loop / reps * 1e6, 2), "identical": one == loop}
+
+
+def reader_threads(device, calls=4000):
+    """Concurrent LsmStorage.get readers (src/lsm_storage.py:153-179: any thread probes a
+    published filter, no lock) on ONE L0 filter (product sizing, sstable.py:274, 100k keys,
+    k = 10): T threads share `calls` may_contain calls; aggregate calls/s for T = 1, 2, 4, 8 and
+    whether every answer equals the single-thread answers.  One-key probes hold the handle's lock
+    shared and run on per-thread reader streams; PBF_SHARED_READERS=0 (set before the library
+    loads) measures the exclusive path."""
+    import threading
+    from pebbledb_amd import BloomFilter
+    from pebbledb_amd.keys import splitmix_hex_keys_str
+    keys = splitmix_hex_keys_str(SEED, 0, 100_000)
+    bf = BloomFilter.build_from_keys_and_fp_rate(keys, 0.001, device=device)
+    probes = splitmix_hex_keys_str(SEED, 50_000, 2000)
+    want = [bf.may_contain(p) for p in probes]
+    out = {"filter_nb_bytes": bf.nb_bytes, "k": bf.nb_hash_functions,
+           "shared_readers": os.environ.get("PBF_SHARED_READERS", "1") != "0"}
+    ok = True
+    for T in (1, 2, 4, 8):
+        res = [None] * T
+        per = calls // T
+        start = threading.Barrier(T + 1)
+
+        def run(t):
+            start.wait()
+            res[t] = [bf.may_contain(probes[(t * per + i) % 2000]) for i in range(per)]
+
+        th = [threading.Thread(target=run, args=(t,)) for t in range(T)]
+        for t in th:
+            t.start()
+        start.wait()
+        t0 = time.perf_counter()
+        for t in th:
+            t.join()
+        dt = time.perf_counter() - t0
+        for t in range(T):
+            ok &= res[t] == [want[(t * per + i) % 2000] for i in range(per)]
+        out[f"threads_{T}_calls_per_s"] = round(T * per / dt)
+    out["identical"] = bool(ok)
+    return out
 
 
 def all_reduce_scalar(torch, dist, value, op, dtype):
@@ -729,6 +771,7 @@ def sst_main(args, rank, world, local, torch, dist, np):
     t0 = time.perf_counter()
     PackedKeys.from_strs(hkeys)
     t_strs = time.perf_counter() - t0
+    compaction = compaction_leg(np, local)
     # CPU baseline: the reference builder's algorithm (oracle restatement), bounded sample
     from oracle import sstable_oracle as so
     cn = 0
@@ -761,8 +804,48 @@ def sst_main(args, rank, world, local, torch, dist, np):
         "cpu_baseline": {"value": round(cn / tc / 1e6, 4), "unit": "Mrecords/s", "cores": 1, "kind": "port",
                          "sample": f"oracle/sstable_oracle.py data_and_meta (the reference builder's algorithm) "
                                    f"on {cn} records in {tc:.1f}s"},
+        "compaction": compaction,
     }
     print(json.dumps(out_line), flush=True)
+
+
+def compaction_leg(np, device, n=4_000_000, vlen=48, max_sstable_size=100_000_000, reps=3):
+    """Compaction's output SSTables (LsmStorage._compact, src/lsm_storage.py:233-251) for a merged
+    run of n records (sorted 16-B hex keys, 48-B values; packed beforehand, as the merging
+    iterator's output would be by the C packer): build_sstables (the split planned on the host,
+    ONE upload, one encode launch for every output, the outputs' filters built side by side on
+    pooled streams) vs one build_sstable call per output over the same ranges, run after run.
+    Host-inclusive (records in host memory -> file bytes of every output); best of `reps`; the
+    files of both paths must be identical."""
+    from pebbledb_amd.keys import PackedKeys, PackedRecords, splitmix_hex_keys
+    from pebbledb_amd.sstable_data import build_sstable, build_sstables, key_offsets, plan_compaction
+    kb = np.sort(splitmix_hex_keys(SEED, 0, n).view("S16").reshape(-1)).view(np.uint8).reshape(n, 16)
+    vals = np.random.default_rng(5).integers(0, 256, n * vlen, dtype=np.uint8)
+    vo = np.arange(n + 1, dtype=np.uint64) * np.uint64(vlen)
+    run = PackedRecords(PackedKeys.fixed(kb), vals, vo, ascii=True)
+    bf, bo, tb, written = plan_compaction(np.asarray(key_offsets(run.keys), np.uint64), vo, 65_536, max_sstable_size)
+    parts = []
+    for t in range(len(tb) - 1):
+        r0, r1 = int(bf[tb[t]]), int(bf[tb[t + 1]])
+        parts.append(PackedRecords(PackedKeys.fixed(kb[r0:r1]), vals[r0 * vlen:r1 * vlen], vo[:r1 - r0 + 1], ascii=True))
+    t_one, t_seq = [], []
+    same = True
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        outs, w = build_sstables(run, max_sstable_size=max_sstable_size, device=device)
+        t_one.append(time.perf_counter() - t0)
+        t0 = time.perf_counter()
+        seq = [build_sstable(p, device=device) for p in parts]
+        t_seq.append(time.perf_counter() - t0)
+        same = same and len(seq) == len(outs) and all(bytes(a[0]) == bytes(b[0]) for a, b in zip(outs, seq))
+        del outs, seq
+    a, b = min(t_one), min(t_seq)
+    return {"records": n, "written": written, "outputs": len(tb) - 1, "max_sstable_size": max_sstable_size,
+            "build_sstables_s": round(a, 4), "build_sstables_Mrecords_s": round(written / a / 1e6, 2),
+            "sequential_build_sstable_s": round(b, 4), "sequential_Mrecords_s": round(written / b / 1e6, 2),
+            "speedup": round(b / a, 3), "files_identical": bool(same),
+            "what": "host-inclusive: packed run -> every output's file bytes (plan, H2D, device encode + filters, "
+                    "D2H, meta, trailer); best of 3"}
 
 
 def spawn_ranks(args) -> int:
@@ -796,14 +879,14 @@ def spawn_ranks(args) -> int:
 
 
 def dist_report(dist, world):
-    """The process group the timing went over: its backend and the world size it saw.  The key
-    is rccl_world_size only when that backend is RCCL ("nccl" on ROCm); a gloo rehearsal reports
-    world_size_seen instead."""
+    """The process group the timing went over: its backend and the world size it saw.
+    `rccl_world_size` is always present (1 for a single-GPU run, the RCCL world otherwise; null
+    for a gloo rehearsal, which is not RCCL); `world_size_seen` is what the group saw."""
     if world == 1:
-        return {"backend": None, "world_size_seen": 1}
+        return {"backend": None, "rccl_world_size": 1, "world_size_seen": 1}
     be = dist.get_backend()
-    key = "rccl_world_size" if be == "nccl" else "world_size_seen"
-    return {"backend": be, key: dist.get_world_size()}
+    ws = dist.get_world_size()
+    return {"backend": be, "rccl_world_size": ws if be == "nccl" else None, "world_size_seen": ws}
 
 
 def dry_run(args, rank, world, dist):

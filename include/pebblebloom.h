@@ -18,10 +18,12 @@
  *     keys_on_device = 1: they are device pointers on the filter's device; the call is
  *     asynchronous on the filter's stream (pbf_stream) and the caller keeps them alive until
  *     pbf_sync (or an event recorded on that stream) completes.
- *   - A handle is one filter on one device with one HIP stream.  Every call takes the handle's
- *     mutex, so one handle may be used from several host threads (the reference builds a
- *     filter under the flush mutex, lsm_storage.py:220, and then probes it from any reader
- *     thread without a lock, lsm_storage.py:153-179); distinct handles run concurrently.
+ *   - A handle is one filter on one device with one HIP stream.  Calls that build, load or
+ *     batch-probe take the handle's lock exclusively; one-key probes (pbf_may_contain,
+ *     pbf_may_contain_set) of a built filter take it SHARED and run on a per-thread reader
+ *     stream, so reader threads probe one filter concurrently (the reference builds a filter
+ *     under the flush mutex, lsm_storage.py:220, and then probes it from any reader thread
+ *     without a lock, lsm_storage.py:153-179); distinct handles run concurrently.
  *   - Working memory of the tiled pipelines and the host staging path is a per-device pool
  *     shared by all handles (pbf_trim releases it), not per-filter: a long-lived filter holds
  *     only its bitmap.
@@ -51,7 +53,8 @@ extern "C" {
 #define PBF_PROBE_DIRECT 1 /* one lane per key, k random word loads, wave ballot */
 #define PBF_PROBE_TILED 2  /* partition (key, position) entries by LDS tile, test in LDS, gather */
 
-/* What the last probe ran (pbf_last_probe_detail): bit flags | (filters per fused gather << 8). */
+/* What the last probe ran (pbf_last_probe_detail): bit flags | (filters per fused gather << 8)
+ * | (tiled pipelines the key batch was split into << 16). */
 #define PBF_DETAIL_RING 1    /* tiled: ring partition (k_part_ring) */
 #define PBF_DETAIL_SORT 2    /* tiled: counting-sort partition (k_part) */
 #define PBF_DETAIL_ONE_KEY 4 /* pbf_may_contain's one-key launch */
@@ -149,6 +152,15 @@ int pbf_popcount(pbf_filter_t* f, uint64_t* out);
 /* Wait for all work queued on the filter's stream. */
 int pbf_sync(pbf_filter_t* f);
 
+/* Stream ordering for device-pointer calls (keys_on_device = 1) without a device-wide sync:
+ * pbf_wait_stream makes the filter's stream wait for everything queued on `stream` so far
+ * (e.g. the torch stream that produced a key batch; NULL = the null stream) -- the next
+ * add / probe of f runs after that producer; pbf_signal_stream makes `stream` wait for
+ * everything queued on the filter's stream so far (a consumer of a device hit mask or bitmap).
+ * Both only enqueue an event record + wait; neither blocks the host. */
+int pbf_wait_stream(pbf_filter_t* f, void* stream);
+int pbf_signal_stream(pbf_filter_t* f, void* stream);
+
 /* The filter's hipStream_t (for events / interop) and its device bitmap (uint32 words). */
 void* pbf_stream(pbf_filter_t* f);
 void* pbf_device_bitmap(pbf_filter_t* f);
@@ -195,6 +207,23 @@ int pbf_encode_data_blocks(int device, const uint8_t* keys, const uint64_t* key_
 int pbf_build_sstable(pbf_filter_t* f, const uint8_t* keys, const uint64_t* key_offsets, const uint8_t* values,
                       const uint64_t* value_offsets, uint64_t n, const uint64_t* block_first, const uint64_t* block_out,
                       uint64_t nblocks, uint8_t* data_out, uint8_t* bitmap_out);
+
+/* Compaction's output SSTables (LsmStorage._compact, src/lsm_storage.py:233-251: a new
+ * SSTableBuilder once current_buffer_position >= max_sstable_size) from ONE upload of the
+ * compacted record run (host memory, offsets start at 0; n records).  The caller plans the split
+ * on the host (pebbledb_amd/sstable_data.plan_compaction): blocks as for pbf_build_sstable but over
+ * the whole run, block_out laid end to end over the outputs' data sections, output t = blocks
+ * [table_blocks[t], table_blocks[t+1]) (table_blocks has ntables+1 entries, 0 .. nblocks; the
+ * plan may end before record n: the reference does not write records left in its last builder's
+ * first open block).  filters[t] is output t's filter (sized by the caller from its key count
+ * with build_from_keys_and_fp_rate's expression, fp 0.001, sstable.py:274), built from its slice
+ * of the SAME device copy of the keys on its own stream; data_outs[t] / bitmap_outs[t]
+ * (bitmap_outs or an entry may be NULL) receive the output's data section and bitmap, the
+ * caller's slices of each SSTable file buffer.  Synchronous. */
+int pbf_build_sstables(pbf_filter_t* const* filters, uint32_t ntables, const uint8_t* keys, const uint64_t* key_offsets,
+                       const uint8_t* values, const uint64_t* value_offsets, uint64_t n, const uint64_t* block_first,
+                       const uint64_t* block_out, uint64_t nblocks, const uint64_t* table_blocks,
+                       uint8_t* const* data_outs, uint8_t* const* bitmap_outs);
 
 /* DataBlockBuilder's greedy blocks (src/blocks.py:78-95, sstable.py:224-244) over n records
  * whose key / value bytes are given by their offsets: block_first[0..nblocks] record indices,

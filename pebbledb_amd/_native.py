@@ -49,6 +49,8 @@ SIGNATURES = {
     "pbf_popcount": (_int, [_vp, ctypes.POINTER(_u64)]),
     "pbf_sync": (_int, [_vp]),
     "pbf_stream": (_vp, [_vp]),
+    "pbf_wait_stream": (_int, [_vp, _vp]),
+    "pbf_signal_stream": (_int, [_vp, _vp]),
     "pbf_device_bitmap": (_vp, [_vp]),
     "pbf_set_build_mode": (_int, [_vp, _int]),
     "pbf_last_build_mode": (_int, [_vp]),
@@ -62,6 +64,7 @@ SIGNATURES = {
     "pbf_scratch_bytes": (_int, [_int, ctypes.POINTER(_u64)]),
     "pbf_encode_data_blocks": (_int, [_int, _u8p, _vp, _u8p, _vp, _u64, _vp, _vp, _u64, _u8p, _int]),
     "pbf_build_sstable": (_int, [_vp, _u8p, _vp, _u8p, _vp, _u64, _vp, _vp, _u64, _u8p, _u8p]),
+    "pbf_build_sstables": (_int, [_vp, _u32, _u8p, _vp, _u8p, _vp, _u64, _vp, _vp, _u64, _vp, _vp, _vp]),
     "pbf_plan_blocks": (_int, [_vp, _vp, _u64, _u64, _vp, _vp, ctypes.POINTER(_u64)]),
     "pbf_key_range_mask": (_int, [_int, _vp, _u8p, _vp, _u32, _u64, _u8p, _vp, _u32, _u8p, _int]),
     "pbf_gen_splitmix_hex": (_int, [_int, _vp, _u8p, _u64, _u64, _u64]),

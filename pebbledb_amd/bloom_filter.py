@@ -298,6 +298,19 @@ class BloomFilter:
         if self._h is not None:
             _native.check(_native.lib().pbf_sync(self._h), "pbf_sync")
 
+    def wait_stream(self, stream: int) -> None:
+        """Order this filter's next device work after everything queued on `stream` (an int
+        hipStream_t, e.g. torch.cuda.current_stream().cuda_stream): a device key batch produced
+        there needs no torch.cuda.synchronize() before add_device / probe_device."""
+        if self._h is not None:
+            _native.check(_native.lib().pbf_wait_stream(self._h, ctypes.c_void_p(stream or None)), "pbf_wait_stream")
+
+    def signal_stream(self, stream: int) -> None:
+        """Make `stream` wait for everything queued on this filter's stream (a consumer of a
+        device hit mask or bitmap)."""
+        if self._h is not None:
+            _native.check(_native.lib().pbf_signal_stream(self._h, ctypes.c_void_p(stream or None)), "pbf_signal_stream")
+
     @property
     def stream(self) -> int:
         """The filter's hipStream_t as an int (torch.cuda.ExternalStream(stream))."""
@@ -325,7 +338,7 @@ class BloomFilter:
 
     @property
     def last_probe_detail(self) -> int:
-        """PBF_DETAIL_* flags of the last probe | (filters per fused gather << 8)."""
+        """PBF_DETAIL_* flags of the last probe | (filters per fused gather << 8) | (tiled pipelines << 16)."""
         return 0 if self._h is None else int(_native.lib().pbf_last_probe_detail(self._h))
 
     @property

@@ -2,6 +2,7 @@
 from __future__ import annotations
 
 import os
+import re
 import subprocess
 import sys
 
@@ -10,9 +11,30 @@ REPO = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libpebblebloom.so")
 SOURCES = [os.path.join(CSRC, "pebblebloom.hip")]
-DEPS = SOURCES + [os.path.join(CSRC, f) for f in ("bloom_kernels.hpp", "murmur_device.hpp", "tiled_kernels.hpp", "ring_kernels.hpp",
-                                                "sstable_kernels.hpp", "lsm_kernels.hpp")] + [
-    os.path.join(REPO, "include", "pebblebloom.h")]
+
+
+def _local_includes(path: str, seen: set) -> None:
+    """Every file a source pulls in by `#include "..."` (transitively), so an edit to any of them
+    marks the library stale and changes source_digest()."""
+    path = os.path.normpath(path)
+    if path in seen:
+        return
+    seen.add(path)
+    with open(path, encoding="utf-8") as fh:
+        for line in fh:
+            m = re.match(r'\s*#\s*include\s*"([^"]+)"', line)
+            if m:
+                _local_includes(os.path.join(os.path.dirname(path), m.group(1)), seen)
+
+
+def _deps() -> list:
+    seen: set = set()
+    for src in SOURCES:
+        _local_includes(src, seen)
+    return sorted(seen)
+
+
+DEPS = _deps()
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("PBF_OFFLOAD_ARCH", "gfx950")
 

@@ -19,6 +19,8 @@
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <shared_mutex>
+#include <atomic>
 #include <string>
 #include <type_traits>
 #include <vector>
@@ -287,15 +289,21 @@ struct pbf_filter {
     TileMap tm{};
     bool tiled_ok = false;
     int probe_mode = PBF_PROBE_AUTO;
-    int last_probe_mode = 0;
-    uint32_t last_probe_detail = 0;  // PBF_DETAIL_* of the last probe
+    std::atomic<int> last_probe_mode{0};          // (written by concurrent readers too)
+    std::atomic<uint32_t> last_probe_detail{0};   // PBF_DETAIL_* of the last probe
     uint32_t last_build_detail = 0;  // PBF_DETAIL_* | (kps / 256) << 12 of the last tiled build
     Scratch* sc = nullptr;           // leased for the current call
     uint64_t* dpop = nullptr;
     hipEvent_t ev = nullptr;       // stream joins of multi-filter probes
+    hipEvent_t wait_ev = nullptr;  // pbf_wait_stream: the caller's stream -> this stream
+    hipEvent_t sig_ev = nullptr;   // pbf_signal_stream: this stream -> the caller's stream
     const char* last_kernel = "";  // the last kernel enqueued on the stream (wait_stream's report)
     bool pending = false;          // work may be queued on the stream since its last completed wait
-    std::mutex mu;                 // one host thread inside the handle at a time
+    // Writers (builds, from_bytes, batch probes: anything that touches the handle's state or
+    // queues work on its stream) hold it exclusively; one-key probes of a built filter hold it
+    // shared and run on a reader stream, so concurrent readers do not queue behind each other
+    // (the reference's get probes a published filter from any thread, lsm_storage.py:153-179).
+    std::shared_mutex mu;
 };
 
 namespace {
@@ -1016,6 +1024,7 @@ int probe_device(pbf_filter_t* f, const Batch& b, uint8_t* hitmask_dev) {
             rc = run_tiled_probe(f, slice(b, i0, std::min<uint64_t>(per, b.n - i0)), hitmask_dev + i0 / 8);
             if (rc) return rc;
         }
+        f->last_probe_detail |= uint32_t(std::min<uint64_t>((b.n + per - 1) / per, 4095)) << 16;
         f->last_probe_mode = PBF_PROBE_TILED;
         return PBF_OK;
     }
@@ -1155,9 +1164,10 @@ int probe_multi_device(pbf_filter_t* const* fs, uint32_t nf, const Batch& b, uin
                 if (rc) return rc;
             }
         }
+        f0->last_probe_detail |= uint32_t(std::min<uint64_t>((b.n + per - 1) / per, 4095)) << 16;
         for (uint32_t i = 0; i < nf; ++i) {
             fs[i]->last_probe_mode = PBF_PROBE_TILED;
-            fs[i]->last_probe_detail = f0->last_probe_detail;
+            fs[i]->last_probe_detail = f0->last_probe_detail.load();
         }
     } else {
         // direct groups by k (in first-appearance order), then the per-filter pipelines
@@ -1333,7 +1343,7 @@ int check_keys(pbf_filter_t* f, const uint8_t* keys, const uint64_t* offsets, ui
 // the run was kept.  Every kernel's loops are bounded and its barriers uniform, and since the
 // blocking wait was replaced by polling no run has hung — but that is not proof, so the wait now
 // reports a stream that does not finish: DESIGN.md §1.)
-int wait_stream(pbf_filter_t* f) {
+int wait_raw(hipStream_t stream, int device, const char* last_kernel) {
     static const long spin_us = [] {
         const char* e = std::getenv("PBF_SPIN_US");
         return e ? std::atol(e) : 200L;
@@ -1348,19 +1358,23 @@ int wait_stream(pbf_filter_t* f) {
     const auto limit = std::chrono::duration<double>(limit_s);
     long nap_us = 10;
     for (;;) {
-        const hipError_t e = hipStreamQuery(f->stream);
-        if (e == hipSuccess) {
-            f->pending = false;
-            return PBF_OK;
-        }
+        const hipError_t e = hipStreamQuery(stream);
+        if (e == hipSuccess) return PBF_OK;
         (void)hipGetLastError();  // "not ready" is not an error (see event_done)
         if (e != hipErrorNotReady) return fail(PBF_ERR_HIP, std::string("hipStreamQuery: ") + hipGetErrorString(e));
         const auto waited = std::chrono::steady_clock::now() - t0;
         if (waited > limit) {
+            // Report, then keep waiting: queued copies may still target host memory the caller
+            // (or this call's stack) owns, and the leased scratch must not be handed back while
+            // kernels still use it.  The call fails only once the stream is idle.
             char msg[256];
             std::snprintf(msg, sizeof msg,
                           "stream %p of device %d did not finish within %.1f s (PBF_WAIT_S); last kernel enqueued: %s",
-                          static_cast<void*>(f->stream), f->device, limit_s, f->last_kernel);
+                          static_cast<void*>(stream), device, limit_s, last_kernel);
+            std::fprintf(stderr, "pebblebloom: %s; waiting for it to drain\n", msg);
+            std::fflush(stderr);
+            const hipError_t se = hipStreamSynchronize(stream);
+            if (se != hipSuccess) (void)hipGetLastError();
             return fail(PBF_ERR_HIP, msg);
         }
         if (waited > spin) {
@@ -1368,6 +1382,12 @@ int wait_stream(pbf_filter_t* f) {
             nap_us = std::min(nap_us * 2, 200L);
         }
     }
+}
+
+int wait_stream(pbf_filter_t* f) {
+    const int rc = wait_raw(f->stream, f->device, f->last_kernel);
+    f->pending = false;  // (also after a timeout: wait_raw returns once the stream has drained)
+    return rc;
 }
 
 #define WAIT(f)                       \
@@ -1381,7 +1401,7 @@ int wait_stream(pbf_filter_t* f) {
 // (the leased scratch, staging, pending modes) must not be shared between two of them.
 #define LOCK(f)                                                         \
     if (!(f)) return fail(PBF_ERR_INVALID, "null filter handle");       \
-    std::lock_guard<std::mutex> lock_((f)->mu)
+    std::unique_lock<std::shared_mutex> lock_((f)->mu)
 
 int add_impl(pbf_filter_t* f, const uint8_t* keys, const uint64_t* offsets, uint32_t key_len, uint64_t n,
              int on_device) {
@@ -1431,7 +1451,7 @@ int probe_multi_impl(pbf_filter_t* const* fs, uint32_t nf, const uint8_t* keys, 
     // every handle of the set, in address order (two overlapping sets cannot deadlock)
     std::vector<pbf_filter_t*> order(fs, fs + nf);
     std::sort(order.begin(), order.end());
-    std::vector<std::unique_lock<std::mutex>> locks;
+    std::vector<std::unique_lock<std::shared_mutex>> locks;
     locks.reserve(nf);
     for (pbf_filter_t* p : order) locks.emplace_back(p->mu);
     int rc = check_keys(fs[0], keys, offsets, key_len, n, offsets != nullptr);
@@ -1545,6 +1565,113 @@ int one_key_stage(int device, OneKeyStage** out) {
     return PBF_OK;
 }
 
+// Streams for one-key probes that hold the filter's lock shared (PBF_READER_STREAMS, default 4
+// = the process's hardware queues): a reader's one-wave kernel does not queue behind another
+// reader's, nor behind a later build on the filter's own stream.  Created once per device; a
+// thread keeps the stream it was dealt.
+hipError_t reader_stream(int device, hipStream_t* out) {
+    static std::mutex mu;
+    static std::map<int, std::vector<hipStream_t>> pools;
+    static std::atomic<uint32_t> next{0};
+    static const size_t nstreams = [] {
+        const char* e = std::getenv("PBF_READER_STREAMS");
+        const int x = e ? std::atoi(e) : 0;
+        return x > 0 ? size_t(std::min(x, 32)) : size_t(4);
+    }();
+    thread_local std::map<int, hipStream_t> mine;
+    auto it = mine.find(device);
+    if (it != mine.end()) {
+        *out = it->second;
+        return hipSuccess;
+    }
+    std::lock_guard<std::mutex> lock(mu);
+    auto& pool = pools[device];
+    while (pool.size() < nstreams) {
+        hipStream_t st = nullptr;
+        const hipError_t e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
+        if (e != hipSuccess) {
+            if (pool.empty()) return e;
+            (void)hipGetLastError();
+            break;
+        }
+        pool.push_back(st);
+    }
+    *out = mine[device] = pool[next++ % pool.size()];
+    return hipSuccess;
+}
+
+// Whether a one-key probe of f may run under f's lock held SHARED: the filter is materialised,
+// nothing of it is still queued on its stream (its last build / from_bytes has completed, so a
+// reader stream sees the finished bitmap), and the key takes the mapped one-key kernel.
+// (PBF_SHARED_READERS=0 sends every one-key probe through the exclusive path: A/B measurements.)
+bool reader_ok(pbf_filter_t* f, uint64_t len) {
+    static const bool enabled = [] {
+        const char* e = std::getenv("PBF_SHARED_READERS");
+        return !(e && e[0] == '0');
+    }();
+    if (!enabled) return false;
+    if (f->k == 0) return true;
+    if (kmax_for(f->k) == 0 || len > kOneKeyMax || f->pristine) return false;
+    if (!f->pending) return true;
+    const hipError_t q = hipStreamQuery(f->stream);
+    if (q != hipSuccess) (void)hipGetLastError();
+    return q == hipSuccess;
+}
+
+// The mapped one-key probe of f on stream s.  shared: the caller holds f's lock shared (reader_ok
+// held), so nothing of the handle is written but the probe diagnostics (atomics).
+int one_key_probe(pbf_filter_t* f, const uint8_t* key, uint64_t len, int* out, hipStream_t s, bool shared) {
+    int rc = PBF_OK;
+    OneKeyStage* st = nullptr;
+    rc = one_key_stage(f->device, &st);
+    if (rc) return rc;
+    // the key and its two offsets go into mapped pinned memory the kernel reads over the bus;
+    // the kernel's hit byte comes back the same way: one launch, no copies
+    uint64_t* offs = reinterpret_cast<uint64_t*>(st->host + kOneKeyOffs);
+    offs[0] = 0;
+    offs[1] = len;
+    if (len) std::memcpy(st->host + kOneKeyData, key, len);
+    st->host[0] = 0xEE;
+    KeySet ks{};
+    ks.data = st->dev + kOneKeyData;
+    ks.offsets = reinterpret_cast<const uint64_t*>(st->dev + kOneKeyOffs);
+    ks.off0 = ks.offsets;
+    dispatch(kmax_for(f->k), kVar, [&](auto KMAX, auto KM) {
+        k_probe<decltype(KMAX)::value, decltype(KM)::value>
+            <<<1, 64, 0, s>>>(ks, 1, int(f->k), f->im, f->bitmap, st->dev, int(f->k));
+    });
+    if (shared) {
+        CHECK_LAUNCH();
+    } else {
+        LAUNCHED(f, "k_probe<one key>");
+    }
+    // The kernel's hit byte lands in mapped host memory as soon as it is stored (the key bytes
+    // were read before it), which is earlier than the stream's completion signal: poll the byte,
+    // and fall back to the stream wait (which also reports a failed kernel) after 2 ms.
+    volatile uint8_t* res = reinterpret_cast<volatile uint8_t*>(st->host);
+    const auto t0 = std::chrono::steady_clock::now();
+    uint8_t hit = 0xEE;
+    for (uint32_t spin = 0;; ++spin) {
+        hit = *res;
+        if (hit != 0xEE) break;
+        if ((spin & 255) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) {
+            if (shared) {
+                rc = wait_raw(s, f->device, "k_probe<one key>");
+                if (rc) return rc;
+            } else {
+                WAIT(f);
+            }
+            hit = *res;
+            break;
+        }
+    }
+    if (hit > 1) return fail(PBF_ERR_HIP, "one-key probe: result byte not written");
+    *out = hit;
+    f->last_probe_mode = PBF_PROBE_DIRECT;
+    f->last_probe_detail = PBF_DETAIL_ONE_KEY;
+    return PBF_OK;
+}
+
 // BloomFilter.may_contain (bloom_filter.py:67-74) for one key; the caller holds f's lock.
 int may_contain_locked(pbf_filter_t* f, const uint8_t* key, uint64_t len, int* out) {
     int rc = enter(f);
@@ -1572,45 +1699,7 @@ int may_contain_locked(pbf_filter_t* f, const uint8_t* key, uint64_t len, int* o
         *out = hm & 1;
         return PBF_OK;
     }
-    OneKeyStage* st = nullptr;
-    rc = one_key_stage(f->device, &st);
-    if (rc) return rc;
-    // the key and its two offsets go into mapped pinned memory the kernel reads over the bus;
-    // the kernel's hit byte comes back the same way: one launch, no copies
-    uint64_t* offs = reinterpret_cast<uint64_t*>(st->host + kOneKeyOffs);
-    offs[0] = 0;
-    offs[1] = len;
-    if (len) std::memcpy(st->host + kOneKeyData, key, len);
-    st->host[0] = 0xEE;
-    KeySet ks{};
-    ks.data = st->dev + kOneKeyData;
-    ks.offsets = reinterpret_cast<const uint64_t*>(st->dev + kOneKeyOffs);
-    ks.off0 = ks.offsets;
-    dispatch(kmax_for(f->k), kVar, [&](auto KMAX, auto KM) {
-        k_probe<decltype(KMAX)::value, decltype(KM)::value>
-            <<<1, 64, 0, f->stream>>>(ks, 1, int(f->k), f->im, f->bitmap, st->dev, int(f->k));
-    });
-    LAUNCHED(f, "k_probe<one key>");
-    // The kernel's hit byte lands in mapped host memory as soon as it is stored (the key bytes
-    // were read before it), which is earlier than the stream's completion signal: poll the byte,
-    // and fall back to the stream wait (which also reports a failed kernel) after 2 ms.
-    volatile uint8_t* res = reinterpret_cast<volatile uint8_t*>(st->host);
-    const auto t0 = std::chrono::steady_clock::now();
-    uint8_t hit = 0xEE;
-    for (uint32_t spin = 0;; ++spin) {
-        hit = *res;
-        if (hit != 0xEE) break;
-        if ((spin & 255) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) {
-            WAIT(f);
-            hit = *res;
-            break;
-        }
-    }
-    if (hit > 1) return fail(PBF_ERR_HIP, "one-key probe: result byte not written");
-    *out = hit;
-    f->last_probe_mode = PBF_PROBE_DIRECT;
-    f->last_probe_detail = PBF_DETAIL_ONE_KEY;
-    return PBF_OK;
+    return one_key_probe(f, key, len, out, f->stream, false);
 }
 
 // The filters' pending work (builds, from_bytes) ordered before work on stream s: a filter
@@ -1634,7 +1723,9 @@ int join_into(pbf_filter_t* f, hipStream_t s) {
 // k_may_contain_set launch per k and 64 filters, the key in and the answer out through mapped
 // pinned memory.  Bit i of out_bits (LSB-first) = filters[i]->may_contain(key).  The caller
 // holds every filter's lock.
-int may_contain_set_locked(pbf_filter_t* const* fs, uint32_t nf, const uint8_t* key, uint64_t len, uint8_t* out_bits) {
+int may_contain_set_locked(pbf_filter_t* const* fs, uint32_t nf, const uint8_t* key, uint64_t len, uint8_t* out_bits,
+                           hipStream_t rs = nullptr) {
+    const bool shared = rs != nullptr;  // every handle held shared, reader_ok for each (no writes)
     pbf_filter_t* f0 = fs[0];
     int rc = enter(f0);
     if (rc) return rc;
@@ -1663,7 +1754,7 @@ int may_contain_set_locked(pbf_filter_t* const* fs, uint32_t nf, const uint8_t* 
     rc = one_key_stage(f0->device, &st);
     if (rc) return rc;
     if (len) std::memcpy(st->host + kOneKeyData, key, len);
-    hipStream_t s = f0->stream;
+    hipStream_t s = shared ? rs : f0->stream;
     for (uint32_t k : ks) {
         std::vector<uint32_t> idx;
         for (uint32_t i = 0; i < nf; ++i)
@@ -1673,10 +1764,12 @@ int may_contain_set_locked(pbf_filter_t* const* fs, uint32_t nf, const uint8_t* 
             fset.nf = uint32_t(std::min<size_t>(kMaxFilterSet, idx.size() - c0));
             for (uint32_t j = 0; j < fset.nf; ++j) {
                 pbf_filter_t* f = fs[idx[c0 + j]];
-                rc = materialise(f);
-                if (rc) return rc;
-                rc = join_into(f, s);
-                if (rc) return rc;
+                if (!shared) {
+                    rc = materialise(f);
+                    if (rc) return rc;
+                    rc = join_into(f, s);
+                    if (rc) return rc;
+                }
                 fset.bm[j] = f->bitmap;
                 fset.im[j] = f->im;
             }
@@ -1687,13 +1780,22 @@ int may_contain_set_locked(pbf_filter_t* const* fs, uint32_t nf, const uint8_t* 
                     k_may_contain_set<decltype(KMAX)::value>
                         <<<1, 64, 0, s>>>(st->dev + kOneKeyData, uint32_t(len), int(k), fset, st->dev);
             });
-            LAUNCHED(f0, "k_may_contain_set");
+            if (shared) {
+                CHECK_LAUNCH();
+            } else {
+                LAUNCHED(f0, "k_may_contain_set");
+            }
             // poll the flag the kernel sets after its answer (earlier than the stream's
             // completion signal); the stream wait (which also reports a failed kernel) after 2 ms
             const auto t0 = std::chrono::steady_clock::now();
             for (uint32_t spin = 0; !*flag; ++spin) {
                 if ((spin & 255) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) {
-                    WAIT(f0);
+                    if (shared) {
+                        rc = wait_raw(s, f0->device, "k_may_contain_set");
+                        if (rc) return rc;
+                    } else {
+                        WAIT(f0);
+                    }
                     if (!*flag) return fail(PBF_ERR_HIP, "one-key set probe: answer not written");
                     break;
                 }
@@ -1702,7 +1804,10 @@ int may_contain_set_locked(pbf_filter_t* const* fs, uint32_t nf, const uint8_t* 
             for (uint32_t j = 0; j < fset.nf; ++j) put(idx[c0 + j], (bits >> j) & 1u);
         }
     }
+    // only the filters k_may_contain_set covered (k == 0 filters were not probed; the others
+    // recorded their own path in may_contain_locked)
     for (uint32_t i = 0; i < nf; ++i) {
+        if (std::find(ks.begin(), ks.end(), fs[i]->k) == ks.end()) continue;
         fs[i]->last_probe_mode = PBF_PROBE_DIRECT;
         fs[i]->last_probe_detail = PBF_DETAIL_ONE_KEY | PBF_DETAIL_SET;
     }
@@ -1774,6 +1879,9 @@ int pbf_create(int device, uint64_t nb_bytes, uint32_t nb_hash_functions, pbf_fi
         }
     }
     if (e == hipSuccess && !f->tiled_ok) f->pristine = false;
+    // the allocation and the zeroing are queued on f's stream: a multi-filter call on another
+    // filter's stream must order after them (join_into)
+    f->pending = true;
     if (e != hipSuccess) {
         std::string msg = std::string("pbf_create: ") + hipGetErrorString(e);
         pbf_destroy(f);
@@ -1795,6 +1903,8 @@ int pbf_destroy(pbf_filter_t* f) {
     if (f->stream) (void)hipStreamSynchronize(f->stream);
     if (f->bitmap) bitmap_release(f->device, bitmap_alloc_bytes(f->alloc_words), f->bitmap);
     if (f->ev) (void)hipEventDestroy(f->ev);
+    if (f->wait_ev) (void)hipEventDestroy(f->wait_ev);
+    if (f->sig_ev) (void)hipEventDestroy(f->sig_ev);
     delete f;  // the stream belongs to the device's pool
     return PBF_OK;
 }
@@ -1974,6 +2084,31 @@ int pbf_sync(pbf_filter_t* f) {
     return wait_stream(f);
 }
 
+int pbf_wait_stream(pbf_filter_t* f, void* stream) {
+    LOCK(f);
+    int rc = enter(f);
+    if (rc) return rc;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (s == f->stream) return PBF_OK;
+    if (!f->wait_ev) HIP_TRY(hipEventCreateWithFlags(&f->wait_ev, hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(f->wait_ev, s));
+    HIP_TRY(hipStreamWaitEvent(f->stream, f->wait_ev, 0));
+    f->pending = true;  // the filter's stream now has (a wait) queued
+    return PBF_OK;
+}
+
+int pbf_signal_stream(pbf_filter_t* f, void* stream) {
+    LOCK(f);
+    int rc = enter(f);
+    if (rc) return rc;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (s == f->stream) return PBF_OK;
+    if (!f->sig_ev) HIP_TRY(hipEventCreateWithFlags(&f->sig_ev, hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(f->sig_ev, f->stream));
+    HIP_TRY(hipStreamWaitEvent(s, f->sig_ev, 0));
+    return PBF_OK;
+}
+
 int pbf_murmur3_x86_32(int device, const uint8_t* key, uint64_t len, uint32_t seed, int32_t* out) {
     if (!out || (len && !key)) return fail(PBF_ERR_INVALID, "null key or out");
     if (len > kOneKeyMax) return fail(PBF_ERR_INVALID, "key longer than 4096 bytes");
@@ -1993,6 +2128,23 @@ int pbf_murmur3_x86_32(int device, const uint8_t* key, uint64_t len, uint32_t se
 }
 
 int pbf_may_contain(pbf_filter_t* f, const uint8_t* key, uint64_t len, int* out) {
+    if (!f) return fail(PBF_ERR_INVALID, "null filter handle");
+    if (!out || (len && !key)) return fail(PBF_ERR_INVALID, "null key or out");
+    {
+        // a built filter: readers share the handle and each runs on its reader stream
+        std::shared_lock<std::shared_mutex> rl(f->mu);
+        if (reader_ok(f, len)) {
+            int rc = enter(f);
+            if (rc) return rc;
+            if (f->k == 0) {  // the AND over no bits (bloom_filter.py:71-74 runs no iteration)
+                *out = 1;
+                return PBF_OK;
+            }
+            hipStream_t rs = nullptr;
+            HIP_TRY(reader_stream(f->device, &rs));
+            return one_key_probe(f, key, len, out, rs, true);
+        }
+    }
     LOCK(f);
     return may_contain_locked(f, key, len, out);
 }
@@ -2009,7 +2161,26 @@ int pbf_may_contain_set(pbf_filter_t* const* filters, uint32_t nfilters, const u
     std::vector<pbf_filter_t*> order(filters, filters + nfilters);
     std::sort(order.begin(), order.end());
     order.erase(std::unique(order.begin(), order.end()), order.end());
-    std::vector<std::unique_lock<std::mutex>> locks;
+    {
+        // built filters: held shared, the launch on the thread's reader stream
+        std::vector<std::shared_lock<std::shared_mutex>> rlocks;
+        rlocks.reserve(order.size());
+        bool ok = true;
+        for (pbf_filter_t* p : order) {
+            rlocks.emplace_back(p->mu);
+            if (!reader_ok(p, len)) {
+                ok = false;
+                break;
+            }
+        }
+        if (ok) {
+            HIP_TRY(hipSetDevice(filters[0]->device));
+            hipStream_t rs = nullptr;
+            HIP_TRY(reader_stream(filters[0]->device, &rs));
+            return may_contain_set_locked(filters, nfilters, key, len, out_bits, rs);
+        }
+    }
+    std::vector<std::unique_lock<std::shared_mutex>> locks;
     locks.reserve(order.size());
     for (pbf_filter_t* p : order) locks.emplace_back(p->mu);
     return may_contain_set_locked(filters, nfilters, key, len, out_bits);
@@ -2043,8 +2214,8 @@ int pbf_set_probe_mode(pbf_filter_t* f, int mode) {
     return PBF_OK;
 }
 
-int pbf_last_probe_mode(pbf_filter_t* f) { return f ? f->last_probe_mode : 0; }
-uint32_t pbf_last_probe_detail(pbf_filter_t* f) { return f ? f->last_probe_detail : 0; }
+int pbf_last_probe_mode(pbf_filter_t* f) { return f ? f->last_probe_mode.load() : 0; }
+uint32_t pbf_last_probe_detail(pbf_filter_t* f) { return f ? f->last_probe_detail.load() : 0u; }
 uint32_t pbf_last_build_detail(pbf_filter_t* f) { return f ? f->last_build_detail : 0; }
 
 int pbf_encode_data_blocks(int device, const uint8_t* keys, const uint64_t* key_offsets, const uint8_t* values,
@@ -2195,6 +2366,147 @@ int pbf_build_sstable(pbf_filter_t* f, const uint8_t* keys, const uint64_t* key_
         HIP_TRY(hipMemcpyAsync(bitmap_out, f->bitmap, f->nb_bytes, hipMemcpyDeviceToHost, s));
     }
     WAIT(f);
+    if (err) return fail(PBF_ERR_INVALID, std::to_string(err) + " block(s) exceed 65536 data bytes");
+    return PBF_OK;
+}
+
+// Compaction's N output SSTables (src/lsm_storage.py:233-251) from ONE upload of the record
+// run: the host plan (pebbledb_amd/sstable_data.plan_compaction: every output's blocks, laid end
+// to end) is encoded by one k_encode_blocks launch for all outputs; output t's filter is built
+// from its slice of the same device keys on its own stream (the filters' streams are dealt
+// round-robin from the device's pool, so up to 8 builds run side by side); the data sections
+// leave on filters[0]'s stream while the filters build.  Synchronous.
+int pbf_build_sstables(pbf_filter_t* const* filters, uint32_t ntables, const uint8_t* keys, const uint64_t* key_offsets,
+                       const uint8_t* values, const uint64_t* value_offsets, uint64_t n, const uint64_t* block_first,
+                       const uint64_t* block_out, uint64_t nblocks, const uint64_t* table_blocks,
+                       uint8_t* const* data_outs, uint8_t* const* bitmap_outs) {
+    if (ntables == 0) return PBF_OK;
+    if (!filters || !keys || !key_offsets || !values || !value_offsets || !block_first || !block_out || !table_blocks ||
+        !data_outs)
+        return fail(PBF_ERR_INVALID, "null pointer");
+    for (uint32_t t = 0; t < ntables; ++t) {
+        if (!filters[t] || !data_outs[t]) return fail(PBF_ERR_INVALID, "null filter or output in the set");
+        if (filters[t]->device != filters[0]->device) return fail(PBF_ERR_INVALID, "the outputs' filters must share a device");
+        for (uint32_t j = 0; j < t; ++j)
+            if (filters[j] == filters[t]) return fail(PBF_ERR_INVALID, "a filter appears twice");
+    }
+    if (key_offsets[0] != 0 || value_offsets[0] != 0) return fail(PBF_ERR_INVALID, "offsets must start at 0");
+    if (nblocks == 0 || block_first[0] != 0 || block_out[0] != 0 || block_first[nblocks] > n)
+        return fail(PBF_ERR_INVALID, "block plan must cover records [0, written) from byte 0");
+    if (table_blocks[0] != 0 || table_blocks[ntables] != nblocks) return fail(PBF_ERR_INVALID, "tables must cover the blocks");
+    for (uint32_t t = 0; t < ntables; ++t)
+        if (table_blocks[t + 1] <= table_blocks[t]) return fail(PBF_ERR_INVALID, "a table without blocks");
+    for (uint64_t b = 0; b < nblocks; ++b) {
+        const uint64_t r0 = block_first[b], r1 = block_first[b + 1];
+        if (r1 <= r0) return fail(PBF_ERR_INVALID, "block plan not increasing");
+        const uint64_t dl = (key_offsets[r1] - key_offsets[r0]) + (value_offsets[r1] - value_offsets[r0]) + 8 * (r1 - r0);
+        if (dl > kMaxBlockData) return fail(PBF_ERR_INVALID, "a block's records exceed 65536 bytes");
+        if (block_out[b + 1] - block_out[b] != dl + 2 * (r1 - r0) + 2)
+            return fail(PBF_ERR_INVALID, "block_out does not match the blocks' encoded sizes");
+    }
+    const uint64_t w = block_first[nblocks];  // records written (the run's tail may be left out)
+    // every handle of the set, in address order
+    std::vector<pbf_filter_t*> order(filters, filters + ntables);
+    std::sort(order.begin(), order.end());
+    std::vector<std::unique_lock<std::shared_mutex>> locks;
+    locks.reserve(ntables);
+    for (pbf_filter_t* p : order) locks.emplace_back(p->mu);
+    pbf_filter_t* f0 = filters[0];
+    int rc = enter(f0);
+    if (rc) return rc;
+    HIP_TRY(allow_lds(k_encode_blocks, kEncodeLds));
+    LEASE(f0);
+    Scratch* sc = f0->sc;
+    hipStream_t s0 = f0->stream;
+    const uint64_t kb = key_offsets[w], vb = value_offsets[w], out_bytes = block_out[nblocks];
+    HIP_TRY(sc->dkeys.ensure(((kb + 15) & ~uint64_t(15)) + 32));
+    HIP_TRY(sc->doffs.ensure((w + 1) * 8));
+    HIP_TRY(sc->svals.ensure(((vb + 15) & ~uint64_t(15)) + 32 + (w + 1) * 8));
+    HIP_TRY(sc->splan.ensure(2 * (nblocks + 1) * 8));
+    HIP_TRY(sc->ssec.ensure(out_bytes + 32));
+    HIP_TRY(sc->serr.ensure(4));
+    auto* dk = static_cast<uint8_t*>(sc->dkeys.p);
+    auto* dko = static_cast<uint64_t*>(sc->doffs.p);
+    auto* dv = static_cast<uint8_t*>(sc->svals.p);
+    auto* dvo = reinterpret_cast<uint64_t*>(dv + ((vb + 15) & ~uint64_t(15)) + 32);
+    auto* dbf = static_cast<uint64_t*>(sc->splan.p);
+    auto* dbo = dbf + nblocks + 1;
+    auto* dsec = static_cast<uint8_t*>(sc->ssec.p);
+    std::vector<void*> registered;
+    auto lock_span = [&](const void* p, uint64_t bytes) {
+        if (bytes < (uint64_t(4) << 20) || is_pinned_host(p)) return;
+        if (hipHostRegister(const_cast<void*>(p), bytes, hipHostRegisterDefault) == hipSuccess)
+            registered.push_back(const_cast<void*>(p));
+        else
+            (void)hipGetLastError();
+    };
+    struct Unregister {
+        std::vector<void*>& v;
+        ~Unregister() {
+            for (void* p : v) (void)hipHostUnregister(p);
+        }
+    } unreg{registered};
+    lock_span(keys, kb);
+    lock_span(values, vb);
+    lock_span(key_offsets, (w + 1) * 8);
+    lock_span(value_offsets, (w + 1) * 8);
+    for (uint32_t t = 0; t < ntables; ++t) {
+        lock_span(data_outs[t], block_out[table_blocks[t + 1]] - block_out[table_blocks[t]]);
+        if (bitmap_outs && bitmap_outs[t]) lock_span(bitmap_outs[t], filters[t]->nb_bytes);
+    }
+    // one H2D of the run; the data blocks of every output and every filter are built from it
+    if (kb) HIP_TRY(hipMemcpyAsync(dk, keys, kb, hipMemcpyHostToDevice, s0));
+    if (vb) HIP_TRY(hipMemcpyAsync(dv, values, vb, hipMemcpyHostToDevice, s0));
+    HIP_TRY(hipMemcpyAsync(dko, key_offsets, (w + 1) * 8, hipMemcpyHostToDevice, s0));
+    HIP_TRY(hipMemcpyAsync(dvo, value_offsets, (w + 1) * 8, hipMemcpyHostToDevice, s0));
+    HIP_TRY(hipMemcpyAsync(dbf, block_first, (nblocks + 1) * 8, hipMemcpyHostToDevice, s0));
+    HIP_TRY(hipMemcpyAsync(dbo, block_out, (nblocks + 1) * 8, hipMemcpyHostToDevice, s0));
+    HIP_TRY(hipMemsetAsync(sc->serr.p, 0, 4, s0));
+    k_encode_blocks<<<uint32_t(nblocks), 512, kEncodeLds, s0>>>(dk, dko, dv, dvo, dbf, dbo, dsec,
+                                                                static_cast<unsigned int*>(sc->serr.p));
+    LAUNCHED(f0, "k_encode_blocks");
+    HIP_TRY(filter_event(f0));
+    HIP_TRY(hipEventRecord(f0->ev, s0));  // the run is on the device
+    // the data sections go back on s0 while the filters build on their own streams
+    for (uint32_t t = 0; t < ntables; ++t) {
+        const uint64_t o0 = block_out[table_blocks[t]], o1 = block_out[table_blocks[t + 1]];
+        HIP_TRY(hipMemcpyAsync(data_outs[t], dsec + o0, o1 - o0, hipMemcpyDeviceToHost, s0));
+    }
+    const Batch all = make_batch(dk, dko, 0, w);
+    for (uint32_t t = 0; t < ntables; ++t) {
+        pbf_filter_t* ft = filters[t];
+        const uint64_t r0 = block_first[table_blocks[t]], r1 = block_first[table_blocks[t + 1]];
+        if (ft != f0 && ft->stream != s0) HIP_TRY(hipStreamWaitEvent(ft->stream, f0->ev, 0));
+        if (ft->k > 0) {  // SSTableBuilder.build's filter over the output's keys (sstable.py:274)
+            if (ft == f0) {
+                rc = add_device(ft, slice(all, r0, r1 - r0));
+            } else {
+                Lease lt(ft);
+                rc = lt.acquire();
+                if (!rc) rc = add_device(ft, slice(all, r0, r1 - r0));
+            }
+            if (rc) return rc;
+        }
+        if (bitmap_outs && bitmap_outs[t]) {
+            rc = materialise(ft);
+            if (rc) return rc;
+            HIP_TRY(hipMemcpyAsync(bitmap_outs[t], ft->bitmap, ft->nb_bytes, hipMemcpyDeviceToHost, ft->stream));
+        }
+        ft->pending = true;
+    }
+    // s0 (whose lease covers the device copy of the run) waits for every build that read it
+    for (uint32_t t = 1; t < ntables; ++t) {
+        pbf_filter_t* ft = filters[t];
+        if (ft->stream == s0) continue;
+        HIP_TRY(filter_event(ft));
+        HIP_TRY(hipEventRecord(ft->ev, ft->stream));
+        HIP_TRY(hipStreamWaitEvent(s0, ft->ev, 0));
+    }
+    unsigned int err = 0;
+    HIP_TRY(hipMemcpyAsync(&err, sc->serr.p, 4, hipMemcpyDeviceToHost, s0));
+    WAIT(f0);
+    for (uint32_t t = 1; t < ntables; ++t)
+        if (filters[t]->pending) WAIT(filters[t]);
     if (err) return fail(PBF_ERR_INVALID, std::to_string(err) + " block(s) exceed 65536 data bytes");
     return PBF_OK;
 }

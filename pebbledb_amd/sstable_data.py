@@ -99,6 +99,64 @@ def plan_blocks_native(ko: np.ndarray, vo: np.ndarray, block_size: int = BLOCK_S
     return bf[:nb.value + 1].copy(), bo[:nb.value + 1].copy()
 
 
+def plan_compaction(ko: np.ndarray, vo: np.ndarray, block_size: int = BLOCK_SIZE,
+                    max_sstable_size: int = 262_144_000):
+    """Compaction's output split (``LsmStorage._compact``, src/lsm_storage.py:233-251) over a
+    record run, on the host block plan.  A builder's position advances only when a data block
+    finishes — when a record does not fit the open block (src/sstable.py:224-268) — and the
+    builder is built as soon as that position reaches max_sstable_size: its last block then holds
+    only the record that finished the previous one.  At the end of the run the last builder is
+    built only if its position is past 0, so records still in its first open block are not
+    written (the reference's behaviour).
+
+    Returns (block_first, block_out, table_blocks, written): blocks as plan_blocks gives them but
+    over the whole run (block_out = offsets in the outputs' data sections laid end to end),
+    table t = blocks [table_blocks[t], table_blocks[t+1]), records [block_first[table_blocks[t]],
+    block_first[table_blocks[t+1]]); `written` = records covered by the outputs."""
+    n = len(ko) - 1
+    if not 0 < block_size <= 65_536:
+        raise ValueError("block_size must be in (0, 65536]: DataBlock offsets are u16 (blocks.py:34)")
+    if n <= 0:
+        return (np.zeros(1, np.uint64), np.zeros(1, np.uint64), np.zeros(1, np.uint64), 0)
+    sizes = (np.diff(ko.astype(np.int64)) + np.diff(vo.astype(np.int64)) + RECORD_HEADER)
+    if int(sizes.max()) > block_size:
+        raise ValueError("a record is larger than block_size (the reference would drop it, blocks.py:84-85)")
+    P = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum(sizes, out=P[1:])
+    first, tables = [0], [0]  # block starts (record index); table starts (block index)
+    s = 0
+    while s < n:
+        pos = 0  # the builder's current_buffer_position
+        split = False
+        while True:
+            e = int(np.searchsorted(P, P[s] + block_size, side="right")) - 1  # block [s, e)
+            if e >= n:
+                break  # the open block: no record arrives to finish it
+            pos += int(P[e] - P[s]) + 2 * (e - s) + 2
+            first.append(e)
+            if pos >= max_sstable_size:  # build(): finish_block() of [e] alone
+                first.append(e + 1)
+                tables.append(len(first) - 1)
+                s = e + 1
+                split = True
+                break
+            s = e
+        if not split:
+            if pos > 0:  # build() at the end: the open block [s, n) is the last one
+                first.append(n)
+                tables.append(len(first) - 1)
+            else:  # _compact's `if current_buffer_position > 0`: [t0, n) is not written
+                first = first[:tables[-1] + 1]
+            break
+    bf = np.asarray(first, dtype=np.uint64)
+    b64 = bf.astype(np.int64)
+    cnt = np.diff(b64)
+    bo = np.zeros(len(bf), dtype=np.uint64)
+    np.cumsum((P[b64[1:]] - P[b64[:-1]]) + 2 * cnt + 2, out=bo[1:])
+    tb = np.asarray(tables, dtype=np.uint64)
+    return bf, bo, tb, int(bf[-1])
+
+
 def encode_data_blocks(pk: PackedKeys, vals: np.ndarray, vo: np.ndarray, block_first: np.ndarray,
                        block_out: np.ndarray, device: int = 0) -> np.ndarray:
     """The data section (every encoded DataBlock back to back), written by the device."""
@@ -188,3 +246,76 @@ def build_sstable(keys, values=None, block_size: int = BLOCK_SIZE, fp_rate: floa
     out[bloom_off + nb_bytes] = k
     out[len(out) - TRAILER:] = np.frombuffer(struct.pack("ii", data_len, bloom_off), dtype=np.uint8)
     return out, metas, bloom
+
+
+def build_sstables(keys, values=None, max_sstable_size: int = 262_144_000, block_size: int = BLOCK_SIZE,
+                   fp_rate: float = 0.001, device=None):
+    """Compaction's output SSTables (``LsmStorage._compact``, src/lsm_storage.py:233-251) for a
+    merged record run: the split of plan_compaction, then every output's data blocks and bloom
+    filter from ONE upload of the run (``pbf_build_sstables``).  `keys` / `values` as for
+    build_sstable (a PackedRecords, or list[str] + list[bytes]).  Returns (outputs, written):
+    outputs = [(file bytes as a uint8 numpy array, meta blocks, filter), ...] in the order
+    _compact returns them, written = records covered (the reference leaves out records still in
+    its last builder's first open block)."""
+    from math import ceil, log
+
+    from .bloom_filter import BloomFilter, _default_device
+    from .sstable_bloom import TRAILER, sstable_size
+
+    dev = _default_device if device is None else int(device)
+    if isinstance(keys, PackedRecords):
+        if values is not None:
+            raise ValueError("PackedRecords carries its values")
+        pk, vals, vo = keys.keys, keys.values, keys.value_offsets
+    else:
+        keys = keys if isinstance(keys, list) else list(keys)
+        pk = PackedKeys.from_strs(keys)
+        vals, vo = pack_values(values)
+    if len(vo) - 1 != pk.n:
+        raise ValueError("keys and values differ in length")
+    ko = np.ascontiguousarray(key_offsets(pk), dtype=np.uint64)
+    vo = np.ascontiguousarray(vo, dtype=np.uint64)
+    bf, bo, tb, written = plan_compaction(ko, vo, block_size, max_sstable_size)
+    nt = len(tb) - 1
+    if nt == 0:
+        return [], written
+    key_src = keys if isinstance(keys, list) else pk
+    files, metas_all, filters, datas, bitmaps, tails = [], [], [], [], [], []
+    for t in range(nt):
+        b0, b1 = int(tb[t]), int(tb[t + 1])
+        n = int(bf[b1] - bf[b0])
+        m = (-n * log(fp_rate)) / (log(2) ** 2)  # bloom_filter.py:109-114, same expression order
+        nb_bytes, k = ceil(m / 8), round((m / n) * log(2))
+        if not 0 <= k <= 255:
+            raise struct.error("ubyte format requires 0 <= number <= 255")
+        base = int(bo[b0])
+        meta, metas = meta_blocks(key_src, bf[b0:b1 + 1], bo[b0:b1 + 1] - np.uint64(base))
+        data_len = int(bo[b1]) - base
+        if data_len + len(meta) > 0x7FFFFFFF:
+            raise struct.error("'i' format requires -2147483648 <= number <= 2147483647")
+        out = np.empty(sstable_size(data_len, len(meta), nb_bytes), dtype=np.uint8)
+        bloom_off = data_len + len(meta)
+        filters.append(BloomFilter(nb_bytes, k, device=dev))
+        files.append(out)
+        metas_all.append(metas)
+        datas.append(out.ctypes.data)
+        bitmaps.append(out.ctypes.data + bloom_off)
+        tails.append((data_len, meta, bloom_off, nb_bytes, k))
+    vp = ctypes.c_void_p
+    hs = (vp * nt)(*[f.handle.value for f in filters])
+    douts = (vp * nt)(*datas)
+    bouts = (vp * nt)(*bitmaps)
+    kbytes = pk.data if pk.data.size else np.zeros(1, np.uint8)
+    vbytes = vals if vals.size else np.zeros(1, np.uint8)
+    bf_c = np.ascontiguousarray(bf, dtype=np.uint64)
+    bo_c = np.ascontiguousarray(bo, dtype=np.uint64)
+    tb_c = np.ascontiguousarray(tb, dtype=np.uint64)
+    rc = _native.lib().pbf_build_sstables(hs, nt, vp(kbytes.ctypes.data), vp(ko.ctypes.data), vp(vbytes.ctypes.data),
+                                          vp(vo.ctypes.data), pk.n, vp(bf_c.ctypes.data), vp(bo_c.ctypes.data),
+                                          len(bf_c) - 1, vp(tb_c.ctypes.data), douts, bouts)
+    _native.check(rc, "pbf_build_sstables")
+    for out, (data_len, meta, bloom_off, nb_bytes, k) in zip(files, tails):
+        out[data_len:bloom_off] = np.frombuffer(meta, dtype=np.uint8)
+        out[bloom_off + nb_bytes] = k
+        out[len(out) - TRAILER:] = np.frombuffer(struct.pack("ii", data_len, bloom_off), dtype=np.uint8)
+    return list(zip(files, metas_all, filters)), written

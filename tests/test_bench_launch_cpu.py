@@ -45,3 +45,27 @@ def test_single_rank_dry_run():
     assert r.returncode == 0, r.stderr[-2000:]
     out = json.loads(r.stdout.strip().splitlines()[-1])
     assert out["n_gpus"] == 1 and out["world_size_seen"] == 1
+
+
+def test_dist_report_keeps_rccl_world_size_key():
+    """The one-GPU JSON keeps `rccl_world_size` (round-3 advice: a gloo-style rename broke the
+    schema of the default run)."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(REPO, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    r = bench.dist_report(None, 1)
+    assert r["rccl_world_size"] == 1 and r["world_size_seen"] == 1
+
+    class G:
+        def __init__(self, be):
+            self.be = be
+
+        def get_backend(self):
+            return self.be
+
+        def get_world_size(self):
+            return 4
+    assert bench.dist_report(G("nccl"), 4)["rccl_world_size"] == 4
+    r = bench.dist_report(G("gloo"), 4)
+    assert r["rccl_world_size"] is None and r["world_size_seen"] == 4

@@ -164,3 +164,99 @@ def test_scratch_is_pooled_not_per_filter(oracle):
     for bf in fs[:3]:
         assert bf.bitmap() == want.tobytes()
         assert bf.may_contain_many(pk).all()
+
+
+def test_shared_readers_beside_a_writer_on_the_same_filter(oracle):
+    """Readers hold a built filter's lock shared (one-key probes on reader streams) while a writer
+    on the SAME handle re-adds keys that are already members and runs batch probes (exclusive);
+    every one-key and set answer equals the oracle's, and the handle records the one-key path."""
+    from pebbledb_amd import may_contain_set
+    n = 40_000
+    pk = PackedKeys.fixed(splitmix_hex_keys(21, 0, n))
+    bf = BloomFilter(2 ** 17, 6)
+    bf.add_many(pk)
+    small = BloomFilter(4099, 3)
+    small.add_many(PackedKeys.fixed(splitmix_hex_keys(21, 0, 1000)))
+    want = oracle.build(2 ** 17, 6, pk)
+    want_small = oracle.build(4099, 3, PackedKeys.fixed(splitmix_hex_keys(21, 0, 1000)))
+    q = PackedKeys.fixed(splitmix_hex_keys(21, n // 2, n))
+    wb = np.unpackbits(oracle.probe(want, 6, q), bitorder="little")[:n]
+    ws = np.unpackbits(oracle.probe(want_small, 3, q), bitorder="little")[:n]
+    qs = _strs(q)
+    errors = []
+    stop = threading.Event()
+
+    def reader(t):
+        try:
+            for i in range(t, n, 53):
+                if bf.may_contain(qs[i]) != bool(wb[i]):
+                    errors.append(("key", t, i))
+                    return
+                if i % 5 == 0:
+                    got = may_contain_set([bf, small, bf], qs[i])
+                    if got != [bool(wb[i]), bool(ws[i]), bool(wb[i])]:
+                        errors.append(("set", t, i, got))
+                        return
+        except Exception as e:  # pragma: no cover
+            errors.append(("exc", t, repr(e)))
+
+    def writer():
+        try:
+            while not stop.is_set():
+                bf.add_many(PackedKeys.fixed(splitmix_hex_keys(21, 0, 2000)))  # members again: no bit changes
+                if not np.array_equal(bf.may_contain_many(q, packed=True)[:100], oracle.probe(want, 6, q)[:100]):
+                    errors.append(("batch",))
+        except Exception as e:  # pragma: no cover
+            errors.append(("wexc", repr(e)))
+
+    w = threading.Thread(target=writer)
+    th = [threading.Thread(target=reader, args=(t,)) for t in range(8)]
+    w.start()
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    stop.set()
+    w.join(timeout=300)
+    assert not errors, errors[:5]
+    assert bf.bitmap() == want.tobytes()
+    assert bf.may_contain(qs[0]) == bool(wb[0]) and bf.last_probe_detail == _native.PBF_DETAIL_ONE_KEY
+
+
+def test_wait_stream_orders_a_torch_producer_without_sync(oracle):
+    """Device keys produced by torch on a side stream (behind a queue of long matmuls, so the copy
+    lands late): pbf_wait_stream orders the filter's add after them with no torch.cuda.synchronize;
+    the bitmap equals the oracle's.  pbf_signal_stream hands the probe's device hit mask back to
+    a torch stream, which reads it without waiting on the host."""
+    torch = pytest.importorskip("torch")
+    n = 300_000
+    host = splitmix_hex_keys(31, 0, n)
+    src = torch.from_numpy(host.reshape(-1)).cuda()
+    torch.cuda.synchronize()
+    side = torch.cuda.Stream()
+    a = torch.randn(4096, 4096, device="cuda")
+    dst = torch.zeros_like(src)
+    with torch.cuda.stream(side):
+        for _ in range(20):  # ~ms of work ahead of the copy on the producer's stream
+            a = a @ a
+            a = a / a.norm()
+        dst.copy_(src)
+    bf = BloomFilter(2 ** 20, 6)
+    bf.set_build_mode(_native.PBF_BUILD_ATOMIC)
+    bf.wait_stream(side.cuda_stream)
+    bf.add_device_fixed(dst.data_ptr(), 16, n)
+    want = oracle.build(2 ** 20, 6, PackedKeys.fixed(host))
+    assert bf.bitmap() == want.tobytes()
+    # consumer side: the hit mask produced on the filter's stream, read on a torch stream
+    q = torch.from_numpy(splitmix_hex_keys(31, n // 2, n).reshape(-1)).cuda()
+    torch.cuda.synchronize()
+    hm = torch.zeros((n + 7) // 8, dtype=torch.uint8, device="cuda")
+    consumer = torch.cuda.Stream()
+    bf.probe_device_fixed(q.data_ptr(), 16, n, hm.data_ptr())
+    bf.signal_stream(consumer.cuda_stream)
+    with torch.cuda.stream(consumer):
+        copy = hm.clone()
+    consumer.synchronize()
+    want_hm = oracle.probe(want, 6, PackedKeys.fixed(splitmix_hex_keys(31, n // 2, n)))
+    assert np.array_equal(copy.cpu().numpy(), want_hm)
+    bf.sync()

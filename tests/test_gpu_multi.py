@@ -239,9 +239,10 @@ def _c5_filters(oracle, nf, n_per, nb=2 ** 27, k=6):
     return fs, want
 
 
-def _c5_probe_and_check(oracle, fs, want, q, nq, k=6, sample=(0, 1_000_000)):
+def _c5_probe_and_check(oracle, fs, want, q, nq, k=6, sample=(0, 1_000_000), samples=None):
     """One device multi-probe of q (nq 16-B keys) against fs; every filter's hit mask equals
-    its own single-filter probe over the whole batch and the oracle's on [sample)."""
+    its own single-filter probe over the whole batch and the oracle's on [sample) (or on each
+    range of `samples`)."""
     nf = len(fs)
     hms = [torch.zeros((nq + 7) // 8, dtype=torch.uint8, device="cuda") for _ in range(nf)]
     torch.cuda.synchronize()
@@ -249,31 +250,36 @@ def _c5_probe_and_check(oracle, fs, want, q, nq, k=6, sample=(0, 1_000_000)):
     fs[0].sync()
     detail = fs[0].last_probe_detail
     got = [h.cpu().numpy() for h in hms]
+    del hms
     single = torch.zeros((nq + 7) // 8, dtype=torch.uint8, device="cuda")
-    a, b = sample
-    a, b = a - a % 8, b - b % 8  # whole hit-mask bytes
-    qh = PackedKeys.fixed(q[a * 16:b * 16].cpu().numpy().reshape(-1, 16))
+    ranges = []
+    for a, b in (samples or [sample]):
+        a, b = max(0, a - a % 8), min(nq, b) - min(nq, b) % 8  # whole hit-mask bytes
+        ranges.append((a, b, PackedKeys.fixed(q[a * 16:b * 16].cpu().numpy().reshape(-1, 16))))
     for f, bf in enumerate(fs):
         single.zero_()
         torch.cuda.synchronize()
         bf.probe_device_fixed(q.data_ptr(), 16, nq, single.data_ptr())
         bf.sync()
         assert np.array_equal(got[f], single.cpu().numpy()), f
-        assert np.array_equal(got[f][a // 8:b // 8], oracle.probe(want[f], k, qh, omp=True)[: (b - a) // 8]), f
+        for a, b, qh in ranges:
+            assert np.array_equal(got[f][a // 8:b // 8], oracle.probe(want[f], k, qh, omp=True)[: (b - a) // 8]), (f, a)
     return got, detail
 
 
-@pytest.mark.timeout(150)
-def test_c5_full_geometry_fused_ring_gather(oracle):
-    """BASELINE.json configs[4] on one GPU as bench.py runs it: 8 filters (nb_bytes = 2^27,
-    k = 6, 10M keys each) and one device multi-probe of 20M + 37 keys (half members spread over
-    the 8 SSTables, half absent): B = 1024 tiles takes the RING partition, the XCD-aware fused
-    tile test and ONE fused k_gather_ring<8> (checked via last_probe_detail).  Every filter's
-    mask == its single probe over the whole batch == the oracle on a 1M-key sample; members all
-    hit; the false-positive count is at the theoretical rate."""
-    nf, n_per = 8, 10_000_000
-    fs, want = _c5_filters(oracle, nf, n_per)
-    nq = 20_000_037
+@pytest.fixture(scope="module")
+def c5_full(oracle):
+    """BASELINE.json configs[4]'s filter set: 8 SSTable filters of nb_bytes = 2^27, k = 6, 10M
+    keys each (built once for the module's full-size C5 tests), plus the oracle's bitmaps."""
+    fs, want = _c5_filters(oracle, 8, 10_000_000)
+    yield fs, want
+    fs.clear()  # the handles go with their last reference
+    torch.cuda.empty_cache()
+
+
+def _c5_queries(nq, nf=8, n_per=10_000_000):
+    """C5's probe batch: the first half members spread evenly over the nf SSTables (filter f's
+    block of `per` keys), the second half absent keys."""
     half = nq // 2
     per = half // nf
     q = torch.empty(nq * 16, dtype=torch.uint8, device="cuda")
@@ -281,12 +287,62 @@ def test_c5_full_geometry_fused_ring_gather(oracle):
         cnt = per if f < nf - 1 else half - (nf - 1) * per
         _dev_hex(SEED, f * n_per, cnt, q, f * per)
     _dev_hex(SEED, nf * n_per, nq - half, q, half)
+    return q, half, per
+
+
+@pytest.mark.timeout(300)
+def test_c5_full_geometry_fused_ring_gather(oracle, c5_full):
+    """BASELINE.json configs[4] on one GPU as bench.py runs it: 8 filters (nb_bytes = 2^27,
+    k = 6, 10M keys each) and one device multi-probe of 20M + 37 keys (half members spread over
+    the 8 SSTables, half absent): B = 1024 tiles takes the RING partition, the XCD-aware fused
+    tile test and ONE fused k_gather_ring<8> (checked via last_probe_detail).  Every filter's
+    mask == its single probe over the whole batch == the oracle on a 1M-key sample; members all
+    hit; the false-positive count is at the theoretical rate."""
+    nf = 8
+    fs, want = c5_full
+    nq = 20_000_037
+    q, half, per = _c5_queries(nq)
     got, detail = _c5_probe_and_check(oracle, fs, want, q, nq, sample=(half - 500_000, half + 500_000))
-    assert detail & _native.PBF_DETAIL_RING and detail >> 8 == nf, hex(detail)
+    assert detail & _native.PBF_DETAIL_RING and (detail >> 8) & 0xFF == nf, hex(detail)
     for f in range(nf):
         bits = np.unpackbits(got[f], bitorder="little")[:nq]
         cnt = per if f < nf - 1 else half - (nf - 1) * per
         assert bits[f * per:f * per + cnt].all(), f
+        fill = fs[f].popcount() / (8 * 2 ** 27)
+        fp = int(bits[half:].sum())
+        assert fp <= 3 * (nq - half) * fill ** 6 + 20, (f, fp)
+
+
+@pytest.mark.timeout(200)
+@pytest.mark.parametrize("nq", [100_000_000, 100_000_037])
+def test_c5_full_size_100m_three_pipelines(oracle, c5_full, nq):
+    """C5 at its own size (BASELINE.json configs[4]: 100M lookup keys vs 8 x 128 MiB filters)
+    under -m gpu.  100M keys take the fused 8-filter path in 3 equal pipelines (the gather's
+    key bitmaps for 8 filters bound a pipeline), the later two offsetting every filter's hit mask
+    by i0 / 8.  Every filter's mask == its own single probe over the whole batch; the oracle
+    agrees on samples straddling both pipeline boundaries and the batch's ragged end for all 8
+    filters; members all hit; false positives at the filters' rate.  The 100_000_037 case is
+    ragged: not a multiple of 8, 64 or 3 x 64."""
+    nf = 8
+    fs, want = c5_full
+    q, half, per = _c5_queries(nq)
+    # pipelines of equal size, multiples of 64 keys (tiled_probe_batch); boundaries in the middle
+    p = 3
+    pl = (((nq + p - 1) // p) + 63) // 64 * 64
+    b1, b2 = pl, 2 * pl
+    samples = [(b1 - 100_000, b1 + 100_000), (b2 - 100_000, b2 + 100_000), (nq - 100_003, nq)]
+    got, detail = _c5_probe_and_check(oracle, fs, want, q, nq, samples=samples)
+    del q
+    assert detail & _native.PBF_DETAIL_RING, hex(detail)
+    assert (detail >> 8) & 0xFF == nf, hex(detail)
+    assert detail >> 16 == p, f"{detail >> 16} pipelines, expected {p} ({hex(detail)})"
+    for f in range(nf):
+        bits = np.unpackbits(got[f], bitorder="little")[:nq]
+        cnt = per if f < nf - 1 else half - (nf - 1) * per
+        assert bits[f * per:f * per + cnt].all(), f
+        # the last byte's padding bits stay clear
+        if nq % 8:
+            assert got[f][-1] >> (nq % 8) == 0, f
         fill = fs[f].popcount() / (8 * 2 ** 27)
         fp = int(bits[half:].sum())
         assert fp <= 3 * (nq - half) * fill ** 6 + 20, (f, fp)
@@ -308,6 +364,6 @@ def test_c5_geometry_small_sets_ragged_and_spills(oracle, nf):
     nq = len(qh)
     q = torch.from_numpy(qh.reshape(-1)).cuda()
     got, detail = _c5_probe_and_check(oracle, fs, want, q, nq, sample=(0, nq // 8 * 8))
-    assert detail & _native.PBF_DETAIL_RING and detail >> 8 == nf, hex(detail)
+    assert detail & _native.PBF_DETAIL_RING and (detail >> 8) & 0xFF == nf, hex(detail)
     b0 = np.unpackbits(got[0], bitorder="little")[:nq]
     assert b0[base:base + 60_000].all()  # the repeated member hits filter 0 every time

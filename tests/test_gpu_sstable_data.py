@@ -101,3 +101,48 @@ def test_device_pointers_and_bad_plans():
     vb2, vo2 = pack_values(big_v)
     with pytest.raises(ValueError):
         encode_data_blocks(pk, vb2, vo2, bad, np.array([0, 10], dtype=np.uint64))
+
+
+# ---------------------------------------------------------------- compaction's output split
+from test_compaction_cpu import CASES as COMPACTION_CASES, case_records  # noqa: E402
+
+
+@pytest.mark.parametrize("case", COMPACTION_CASES, ids=[c["name"] for c in COMPACTION_CASES])
+def test_build_sstables_equals_reference_compaction(case):
+    """build_sstables (one upload, one encode launch for every output, the filters on their own
+    streams) writes the files the REAL reference's _compact wrote (tests/golden/
+    compaction_split.json): the same number of SSTables, each byte for byte (sha256), the same
+    records left out at the end; each output also equals build_sstable of its record range."""
+    from pebbledb_amd.sstable_data import build_sstables
+    keys, vals = case_records(case)
+    outs, written = build_sstables(keys, vals, case["max_sstable_size"], case["block_size"])
+    assert written == case["records_written"]
+    assert len(outs) == len(case["outputs"])
+    for (f, metas, bloom), o in zip(outs, case["outputs"]):
+        assert len(f) == o["file_len"]
+        assert hashlib.sha256(bytes(f)).hexdigest() == o["file_sha256"], o["first_record"]
+        assert (bloom.nb_bytes, bloom.nb_hash_functions) == (o["nb_bytes"], o["k"])
+        one, _, _ = build_sstable(keys[o["first_record"]:o["end_record"]], vals[o["first_record"]:o["end_record"]],
+                                  case["block_size"])
+        assert bytes(one) == bytes(f)
+
+
+def test_build_sstables_packed_large_run(oracle):
+    """A flush-scale run through PackedRecords: 400k records of 16-B keys + 40..103-B values,
+    64 KiB blocks, 6 MB outputs (5 tables, filters built concurrently on pooled streams): every
+    output equals build_sstable of its range, and its bitmap equals the C oracle's."""
+    from pebbledb_amd.sstable_data import build_sstables, plan_compaction
+    from pebbledb_amd.keys import splitmix_hex_keys_str
+    n = 400_000
+    keys = sorted(splitmix_hex_keys_str(77, 0, n))
+    vals = [bytes(((i * 131 + j * 29) & 0xFF) for j in range(40 + i % 64)) for i in range(n)]
+    recs = PackedRecords.from_iter(zip(keys, vals))
+    outs, written = build_sstables(recs, max_sstable_size=6_000_000)
+    bf, bo, tb, w = plan_compaction(np.asarray(key_offsets(recs.keys), np.uint64), recs.value_offsets, 65536, 6_000_000)
+    assert written == w and len(outs) == len(tb) - 1 >= 4
+    for t, (f, metas, bloom) in enumerate(outs):
+        r0, r1 = int(bf[tb[t]]), int(bf[tb[t + 1]])
+        one, _, b1 = build_sstable(keys[r0:r1], vals[r0:r1])
+        assert bytes(one) == bytes(f), t
+        want = oracle.build(bloom.nb_bytes, bloom.nb_hash_functions, PackedKeys.from_strs(keys[r0:r1]), omp=True)
+        assert bloom.bitmap() == want.tobytes(), t
