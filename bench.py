@@ -524,6 +524,12 @@ def sets_main(args, rank, world, local, torch, dist, np):
             b_pass *= len(mine)
             pass_ms = ms
         ach = b_pass / (pass_ms * 1e-3) / 1e9
+        # PMC traffic of the same pass (profiles/traffic_c4.json: one filter's build pass, so x the
+        # rank's filters; profiles/traffic_c5.json: the multi-filter probe, already x its pipelines)
+        tr = measured_traffic(args.config)
+        traffic = None
+        if tr is not None:
+            traffic = int(tr["build"] * len(mine)) if args.config == "c4" else int(tr["probe"])
         out = {
             "metric": metric, "value": round(unit_total / (ms * 1e-3) / 1e6, 3),
             "unit": unit, "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 4),
@@ -532,8 +538,9 @@ def sets_main(args, rank, world, local, torch, dist, np):
             "config": {"workload": what, "nb_bytes": nb_bytes, "k": k, "filters_per_rank": len(mine),
                        "parallelism": f"filters-over-gpus x{world}"},
             "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "kernel": pk,
-                         "algorithmic_bytes": int(b_pass), "avg_ms": round(pass_ms, 4)},
+                         "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": pk,
+                         "algorithmic_bytes": int(b_pass), "avg_ms": round(pass_ms, 4),
+                         "traffic_source": tr["source"] if tr else None},
             "check": {"members_all_hit": ok},
             **dist_report(dist, world),
         }

@@ -96,8 +96,10 @@ int pbf_probe(pbf_filter_t* f, const uint8_t* keys, const uint64_t* offsets, uin
 /* LsmStorage.get's filter checks for a batch of keys against several SSTable filters
  * (src/lsm_storage.py:164-169 L0 newest-first, :173-175 per level): hitmasks[i] receives
  * may_contain over the batch for filters[i], ceil(n/8) bytes LSB-first, host or device memory as
- * keys_on_device says (hitmasks itself is a host array of nfilters pointers).  All filters
- * must be on one device and distinct.  When they share (nb_bytes, k) and are large (the tiled
+ * keys_on_device says (hitmasks itself is a host array of nfilters pointers).  Filters must be
+ * distinct; with keys_on_device = 1 they must share one device, while a HOST batch over filters
+ * on several devices fans out to one host thread per device (pbf_probe_multi_placed, grouped by
+ * device).  When they share (nb_bytes, k) and are large (the tiled
  * probe) the keys are hashed and partitioned once for up to 8 filters and only the tile test
  * and gather run per filter.  Otherwise -- SSTable filters of mixed sizes, the usual LSM case
  * (each sized from its own key count, sstable.py:274) -- the filters whose own probe is direct
@@ -110,6 +112,17 @@ int pbf_probe_multi_fixed(pbf_filter_t* const* filters, uint32_t nfilters, const
                           uint64_t n, uint8_t* const* hitmasks, int keys_on_device);
 int pbf_probe_multi(pbf_filter_t* const* filters, uint32_t nfilters, const uint8_t* keys, const uint64_t* offsets,
                     uint64_t n, uint8_t* const* hitmasks, int keys_on_device);
+
+/* The host-batch multi-probe over a filter set placed on several devices from one process (an
+ * LSM's SSTable filters spread one per GPU; LsmStorage.get, src/lsm_storage.py:164-179):
+ * group_of[i] names filter i's placement group (filters of one group must share a device; a
+ * device may hold several groups).  Each group runs pbf_probe_multi on its own host thread,
+ * staging the batch to its device itself (a replicated H2D); hitmasks[i] receives filter i's
+ * mask, so the masks come back in the caller's (get) order.  offsets == NULL: fixed key_len.
+ * Synchronous. */
+int pbf_probe_multi_placed(pbf_filter_t* const* filters, uint32_t nfilters, const uint32_t* group_of,
+                           const uint8_t* keys, const uint64_t* offsets, uint32_t key_len, uint64_t n,
+                           uint8_t* const* hitmasks);
 
 /* BloomFilter.may_contain(key) for ONE key (bloom_filter.py:67-74), the per-key call of
  * LsmStorage.get (lsm_storage.py:165,175): key is host memory (UTF-8 bytes, len may be 0),
@@ -151,6 +164,13 @@ int pbf_popcount(pbf_filter_t* f, uint64_t* out);
 
 /* Wait for all work queued on the filter's stream. */
 int pbf_sync(pbf_filter_t* f);
+
+/* The device index map of a filter of nb_bytes (host-side, no GPU): how `hash % bits_size`
+ * (Python floor-mod of the signed hash, bloom_filter.py:47) is computed for m = 8*nb_bytes.
+ * mode 0: m a power of two <= 2^32, u32(h) & (m-1); 1: m < 2^30, a mod m = a - (mulhi(a, magic)
+ * >> shift) * m for a = h >= 0 ? h : ~h; 2: m >= 2^31, h or h + m; 3: 2^30 < m < 2^31, one
+ * conditional subtract.  Exposed so the reciprocal can be checked exhaustively on the host. */
+int pbf_index_params(uint64_t nb_bytes, uint32_t* mode, uint64_t* magic, uint32_t* shift);
 
 /* Stream ordering for device-pointer calls (keys_on_device = 1) without a device-wide sync:
  * pbf_wait_stream makes the filter's stream wait for everything queued on `stream` so far

@@ -42,6 +42,7 @@ SIGNATURES = {
     "pbf_probe": (_int, [_vp, _u8p, _vp, _u64, _u8p, _int]),
     "pbf_probe_multi_fixed": (_int, [_vp, _u32, _u8p, _u32, _u64, _vp, _int]),
     "pbf_probe_multi": (_int, [_vp, _u32, _u8p, _vp, _u64, _vp, _int]),
+    "pbf_probe_multi_placed": (_int, [_vp, _u32, _vp, _u8p, _vp, _u32, _u64, _vp]),
     "pbf_hash_indices_fixed": (_int, [_vp, _u8p, _u32, _u64, _vp, _int]),
     "pbf_hash_indices": (_int, [_vp, _u8p, _vp, _u64, _vp, _int]),
     "pbf_get_bitmap": (_int, [_vp, _u8p, _u64]),
@@ -49,6 +50,7 @@ SIGNATURES = {
     "pbf_popcount": (_int, [_vp, ctypes.POINTER(_u64)]),
     "pbf_sync": (_int, [_vp]),
     "pbf_stream": (_vp, [_vp]),
+    "pbf_index_params": (_int, [_u64, ctypes.POINTER(_u32), ctypes.POINTER(_u64), ctypes.POINTER(_u32)]),
     "pbf_wait_stream": (_int, [_vp, _vp]),
     "pbf_signal_stream": (_int, [_vp, _vp]),
     "pbf_device_bitmap": (_vp, [_vp]),

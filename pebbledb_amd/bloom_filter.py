@@ -382,11 +382,14 @@ def _native_set(filters):
     return native
 
 
-def may_contain_multi(filters, keys) -> np.ndarray:
+def may_contain_multi(filters, keys, groups=None) -> np.ndarray:
     """``may_contain`` of every key against every filter, the batched form of
     ``LsmStorage.get``'s filter checks (src/lsm_storage.py:164-175).  Returns a uint8 matrix
-    [len(filters), ceil(n/8)] of LSB-first hit masks.  Filters must share a device; when they
-    also share (nb_bytes, k) the keys are hashed and partitioned once (pbf_probe_multi)."""
+    [len(filters), ceil(n/8)] of LSB-first hit masks, row i = filters[i] (the get order).  Filters
+    of one device that share (nb_bytes, k) are hashed and partitioned once (pbf_probe_multi);
+    filters on several devices (or `groups`: a placement-group id per filter, filters of one group
+    on one device) are probed by one host thread per group, each staging the batch to its own
+    device (pbf_probe_multi_placed)."""
     filters = list(filters)
     pk = keys if isinstance(keys, PackedKeys) else PackedKeys.from_strs(list(keys))
     nbm = (pk.n + 7) // 8
@@ -402,7 +405,11 @@ def may_contain_multi(filters, keys) -> np.ndarray:
         hs = (ctypes.c_void_p * len(native))(*[filters[i]._h.value for i in native])
         outs = (ctypes.c_void_p * len(native))(*[out[i].ctypes.data for i in native])
         L = _native.lib()
-        if pk.key_len > 0:
+        if groups is not None:
+            gs = np.ascontiguousarray([int(groups[i]) for i in native], dtype=np.uint32)
+            rc = L.pbf_probe_multi_placed(hs, len(native), _vp(gs), _vp(pk.data),
+                                          None if pk.key_len > 0 else _vp(pk.offsets), pk.key_len, pk.n, outs)
+        elif pk.key_len > 0:
             rc = L.pbf_probe_multi_fixed(hs, len(native), _vp(pk.data), pk.key_len, pk.n, outs, 0)
         else:
             rc = L.pbf_probe_multi(hs, len(native), _vp(pk.data), _vp(pk.offsets), pk.n, outs, 0)
@@ -413,20 +420,22 @@ def may_contain_multi(filters, keys) -> np.ndarray:
 def may_contain_set(filters, key: str) -> list[bool]:
     """``filters[i].may_contain(key)`` for every filter, in ONE launch per k (pbf_may_contain_set):
     the per-key form of LsmStorage.get's bloom checks over its L0 and in-range level SSTables
-    (src/lsm_storage.py:164-179).  Filters may have any sizes; they must share a device."""
+    (src/lsm_storage.py:164-179).  Filters may have any sizes; filters on several devices take
+    one launch per device."""
     filters = list(filters)
     if not filters:
         return []
     native = _native_set(filters)
     res = [True] * len(filters)  # k == 0: the AND over no bits
-    if native:
-        enc = key.encode("utf-8")
-        hs = (ctypes.c_void_p * len(native))(*[filters[i]._h.value for i in native])
-        out = np.zeros((len(native) + 7) // 8, dtype=np.uint8)
-        _native.check(_native.lib().pbf_may_contain_set(hs, len(native), enc, len(enc), _vp(out)),
+    enc = key.encode("utf-8")
+    for dev in dict.fromkeys(filters[i].device for i in native):  # one launch per device
+        idx = [i for i in native if filters[i].device == dev]
+        hs = (ctypes.c_void_p * len(idx))(*[filters[i]._h.value for i in idx])
+        out = np.zeros((len(idx) + 7) // 8, dtype=np.uint8)
+        _native.check(_native.lib().pbf_may_contain_set(hs, len(idx), enc, len(enc), _vp(out)),
                       "pbf_may_contain_set")
         bits = np.unpackbits(out, bitorder="little")
-        for j, i in enumerate(native):
+        for j, i in enumerate(idx):
             res[i] = bool(bits[j])
     return res
 

@@ -36,7 +36,7 @@ struct KeySet {
 template <int KMAX, int KM, class Emit>
 __device__ __forceinline__ void hash_key(const KeySet& ks, uint64_t i, int k, Emit&& emit, int sbase = 0) {
     if constexpr (KM == kFixed16) {
-        const uint4 w = reinterpret_cast<const uint4*>(ks.data)[i];
+        const uint4 w = gld(reinterpret_cast<const uint4*>(ks.data) + i);
         if constexpr (KMAX == 0) {
             murmur_seeds_loop(ks.data + i * 16, 16u, k, emit, sbase);
         } else {
@@ -49,9 +49,9 @@ __device__ __forceinline__ void hash_key(const KeySet& ks, uint64_t i, int k, Em
             p = ks.data + i * uint64_t(ks.key_len);
             len = ks.key_len;
         } else {
-            const uint64_t ob = *ks.off0;
-            const uint64_t a = ks.offsets[i] - ob;
-            const uint64_t b = ks.offsets[i + 1] - ob;
+            const uint64_t ob = gld(ks.off0);
+            const uint64_t a = gld(ks.offsets + i) - ob;
+            const uint64_t b = gld(ks.offsets + i + 1) - ob;
             p = ks.data + a;
             len = uint32_t(b - a);
         }

@@ -16,6 +16,31 @@ constexpr uint32_t kC2 = 0x1b873593u;
 
 __device__ __forceinline__ uint32_t rotl32(uint32_t x, int r) { return __builtin_rotateleft32(x, r); }
 
+// A load through the global address space.  Key bytes and offsets (device memory, or mapped
+// pinned host memory for the one-key probes) reach the kernels through generic pointers, which
+// the compiler loads with flat_* instructions; a flat load's wait also drains every outstanding
+// LDS operation (s_waitcnt vmcnt(0) lgkmcnt(0)), which in the partitions serialises the hash's
+// key loads with the LDS atomics of the previous keys' positions.  The integer -> global pointer
+// cast makes them global_load_*.
+template <class T>
+__device__ __forceinline__ T gld(const T* p) {
+#ifdef PBF_AB_FLAT  // A/B only (round 4): the generic (flat) loads this replaces
+    return *p;
+#else
+    return *(const __attribute__((address_space(1))) T*)(reinterpret_cast<uintptr_t>(p));
+#endif
+}
+// (HIP's uint4 cannot be copied out of an address-space-qualified lvalue: load the vector type)
+__device__ __forceinline__ uint4 gld(const uint4* p) {
+#ifdef PBF_AB_FLAT
+    return *p;
+#else
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    const v4u x = *(const __attribute__((address_space(1))) v4u*)(reinterpret_cast<uintptr_t>(p));
+    return make_uint4(x.x, x.y, x.z, x.w);
+#endif
+}
+
 __device__ __forceinline__ uint32_t mix_block(uint32_t k) {
     k *= kC1;
     k = rotl32(k, 15);
@@ -49,9 +74,9 @@ __device__ __forceinline__ uint32_t load_u32_any(const uint8_t* p) {
     const uintptr_t a = reinterpret_cast<uintptr_t>(p);
     const uint32_t* q = reinterpret_cast<const uint32_t*>(a & ~uintptr_t(3));
     const uint32_t sh = uint32_t(a & 3);
-    const uint32_t lo = q[0];
+    const uint32_t lo = gld(q);
     if (sh == 0) return lo;
-    const uint32_t hi = q[1];
+    const uint32_t hi = gld(q + 1);
     return __builtin_amdgcn_alignbyte(hi, lo, sh);
 }
 
@@ -60,8 +85,8 @@ __device__ __forceinline__ uint32_t load_tail(const uint8_t* p, uint32_t t) {
     const uintptr_t a = reinterpret_cast<uintptr_t>(p);
     const uint32_t* q = reinterpret_cast<const uint32_t*>(a & ~uintptr_t(3));
     const uint32_t sh = uint32_t(a & 3);
-    const uint32_t lo = q[0];
-    const uint32_t hi = (sh + t > 4) ? q[1] : 0u;
+    const uint32_t lo = gld(q);
+    const uint32_t hi = (sh + t > 4) ? gld(q + 1) : 0u;
     const uint32_t v = __builtin_amdgcn_alignbyte(hi, lo, sh);
     return v & ((1u << (8 * t)) - 1u);
 }
@@ -91,7 +116,7 @@ __device__ __forceinline__ void murmur_seeds_seg(const uint8_t* p, uint32_t len,
         uint32_t W[20];
 #pragma unroll
         for (int c = 0; c < 5; ++c) {
-            const uint4 v = base[min(4 * seg + c, nchunks - 1)];
+            const uint4 v = gld(base + min(4 * seg + c, nchunks - 1));
             W[4 * c] = v.x;
             W[4 * c + 1] = v.y;
             W[4 * c + 2] = v.z;
@@ -159,34 +184,43 @@ __device__ __forceinline__ void murmur_seeds_loop(const uint8_t* p, uint32_t len
 
 // ---------------------------------------------------------------- Python floor-mod index
 // idx = h % m with h the SIGNED int32 hash and Python's floor semantics (result in [0, m)).
+// For m < 2^31 write a = h >= 0 ? h : ~h (a < 2^31); then idx = h >= 0 ? a mod m : m-1-(a mod m).
 enum IndexMode : uint32_t {
     kPow2 = 0,   // m a power of two, m <= 2^32: idx = u32(h) & (m-1)
-    kSmall = 1,  // m < 2^31: a = h>=0 ? h : ~h (< 2^31); r = a mod m; idx = h>=0 ? r : m-1-r
+    kSmall = 1,  // m < 2^30: a mod m by a 32-bit reciprocal (below)
     kLarge = 2,  // m >= 2^31: |h| <= 2^31 <= m, so idx = h>=0 ? h : h + m (64-bit)
+    kNear = 3,   // 2^30 < m < 2^31: a < 2^31 < 2m, so a mod m = a >= m ? a - m : a (no multiply)
 };
 
 struct IndexMap {
     uint64_t m;      // bits_size = 8 * nb_bytes
-    uint64_t magic;  // Lemire fastmod constant for kSmall: floor((2^64-1)/m) + 1
+    uint64_t magic;  // kSmall: M = ceil(2^(31+l) / m), l = ceil(log2 m) (M < 2^32)
     uint32_t mode;
-    uint32_t mask;   // m-1 for kPow2
+    uint32_t mask;   // kPow2: m-1; kSmall: the shift l-1
 };
 
-// a mod d for a, d < 2^32 (Lemire, Kaser & Kurz, "Faster remainder by direct computation").
-__device__ __forceinline__ uint32_t fastmod_u32(uint32_t a, uint64_t magic, uint32_t d) {
-    const uint64_t low = magic * uint64_t(a);
-    return uint32_t(__umul64hi(low, uint64_t(d)));
+// a mod m for a < 2^31, m < 2^30 not a power of two: q = floor(a / m) = mulhi(a, M) >> (l-1)
+// (Granlund & Montgomery, "Division by invariant integers using multiplication", Thm 4.2 with
+// N = 31: 2^(31+l) <= M*m < 2^(31+l) + m <= 2^(31+l) + 2^l), r = a - q*m.  Two quarter-rate
+// multiplies instead of the six of a 64-bit Lemire fastmod (C4's product-sized filters hash 10
+// positions per key through this).
+__device__ __forceinline__ uint32_t mod_small(uint32_t a, uint32_t magic, uint32_t shift, uint32_t m) {
+    const uint32_t q = __umulhi(a, magic) >> shift;
+    return a - q * m;
 }
 
 __device__ __forceinline__ uint64_t py_index(uint32_t hu, const IndexMap& im) {
     const int32_t h = int32_t(hu);
     if (im.mode == kPow2) return uint64_t(hu & im.mask);
-    if (im.mode == kSmall) {
-        const uint32_t a = h >= 0 ? hu : ~hu;
-        const uint32_t r = fastmod_u32(a, im.magic, uint32_t(im.m));
-        return h >= 0 ? uint64_t(r) : uint64_t(uint32_t(im.m) - 1u - r);
-    }
-    return h >= 0 ? uint64_t(hu) : uint64_t(int64_t(h) + int64_t(im.m));
+    if (im.mode == kLarge) return h >= 0 ? uint64_t(hu) : uint64_t(int64_t(h) + int64_t(im.m));
+    const uint32_t m = uint32_t(im.m);
+    const uint32_t a = h >= 0 ? hu : ~hu;
+#ifdef PBF_AB_LEMIRE_INDEX  // A/B only (round 4): the previous 64-bit Lemire fastmod for every m < 2^31
+    const uint32_t r = uint32_t(__umul64hi(im.magic * uint64_t(a), uint64_t(m)));
+#else
+    const uint32_t r = im.mode == kNear ? (a >= m ? a - m : a) : mod_small(a, uint32_t(im.magic), im.mask, m);
+#endif
+    return h >= 0 ? uint64_t(r) : uint64_t(m - 1u - r);
 }
 
 }  // namespace pbf

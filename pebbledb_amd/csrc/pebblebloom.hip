@@ -182,9 +182,20 @@ IndexMap make_index_map(uint64_t m) {
     if (pow2 && m <= (uint64_t(1) << 32)) {
         im.mode = kPow2;
         im.mask = uint32_t(m - 1);
+#ifdef PBF_AB_LEMIRE_INDEX
     } else if (m < (uint64_t(1) << 31)) {
         im.mode = kSmall;
         im.magic = ~uint64_t(0) / m + 1;
+#endif
+    } else if (m < (uint64_t(1) << 30)) {
+        // mod_small's reciprocal: l = ceil(log2 m), M = ceil(2^(31+l) / m) < 2^32, shift l-1
+        uint32_t l = 0;
+        while ((uint64_t(1) << l) < m) ++l;
+        im.mode = kSmall;
+        im.magic = ((uint64_t(1) << (31 + l)) + m - 1) / m;
+        im.mask = l - 1;
+    } else if (m < (uint64_t(1) << 31)) {
+        im.mode = kNear;
     } else {
         im.mode = kLarge;
     }
@@ -1476,6 +1487,46 @@ int probe_multi_impl(pbf_filter_t* const* fs, uint32_t nf, const uint8_t* keys, 
     return PBF_OK;
 }
 
+// A filter set spread over several placement groups (LsmStorage.get's filters placed one per GPU,
+// src/lsm_storage.py:164-179): each group — filters of one device — is probed by probe_multi_impl
+// on its own host thread, every group staging the host key batch to its own device (a replicated
+// H2D), its hit masks written to the caller's buffers at the filters' own places in the set (the
+// get order).  The calling thread runs the first group.  Host keys and hit masks only.
+int probe_multi_groups(pbf_filter_t* const* fs, uint32_t nf, const uint32_t* group_of, const uint8_t* keys,
+                       const uint64_t* offsets, uint32_t key_len, uint64_t n, uint8_t* const* hitmasks) {
+    std::vector<uint32_t> ids;  // distinct groups in first-appearance order
+    for (uint32_t i = 0; i < nf; ++i) {
+        if (!fs[i]) return fail(PBF_ERR_INVALID, "null filter handle in set");
+        for (uint32_t j = 0; j < i; ++j)
+            if (fs[j] == fs[i]) return fail(PBF_ERR_INVALID, "a filter appears twice in the set");
+        if (std::find(ids.begin(), ids.end(), group_of[i]) == ids.end()) ids.push_back(group_of[i]);
+    }
+    const size_t G = ids.size();
+    std::vector<std::vector<pbf_filter_t*>> gfs(G);
+    std::vector<std::vector<uint8_t*>> ghm(G);
+    for (uint32_t i = 0; i < nf; ++i) {
+        const size_t g = size_t(std::find(ids.begin(), ids.end(), group_of[i]) - ids.begin());
+        if (!gfs[g].empty() && gfs[g][0]->device != fs[i]->device)
+            return fail(PBF_ERR_INVALID, "the filters of one placement group must share a device");
+        gfs[g].push_back(fs[i]);
+        ghm[g].push_back(hitmasks[i]);
+    }
+    std::vector<int> rcs(G, PBF_OK);
+    std::vector<std::string> errs(G);
+    auto run = [&](size_t g) {
+        rcs[g] = probe_multi_impl(gfs[g].data(), uint32_t(gfs[g].size()), keys, offsets, key_len, n, ghm[g].data(), 0);
+        if (rcs[g]) errs[g] = g_last_error;
+    };
+    std::vector<std::thread> th;
+    th.reserve(G);
+    for (size_t g = 1; g < G; ++g) th.emplace_back(run, g);
+    run(0);
+    for (auto& t : th) t.join();
+    for (size_t g = 0; g < G; ++g)
+        if (rcs[g]) return fail(rcs[g], "placement group " + std::to_string(ids[g]) + ": " + errs[g]);
+    return PBF_OK;
+}
+
 int hash_impl(pbf_filter_t* f, const uint8_t* keys, const uint64_t* offsets, uint32_t key_len, uint64_t n,
               uint64_t* out, int on_device) {
     LOCK(f);
@@ -2007,17 +2058,57 @@ int pbf_probe(pbf_filter_t* f, const uint8_t* keys, const uint64_t* offsets, uin
     return probe_impl(f, keys ? keys : reinterpret_cast<const uint8_t*>(offsets), offsets, 0, n, hitmask, on_device);
 }
 
+// Host batches over filters on several devices fan out to one host thread per device.
+static bool multi_device(pbf_filter_t* const* fs, uint32_t nf) {
+    for (uint32_t i = 1; i < nf; ++i)
+        if (fs[i] && fs[0] && fs[i]->device != fs[0]->device) return true;
+    return false;
+}
+
+static int by_device(pbf_filter_t* const* fs, uint32_t nf, std::vector<uint32_t>& group_of) {
+    group_of.resize(nf);
+    for (uint32_t i = 0; i < nf; ++i) {
+        if (!fs[i]) return fail(PBF_ERR_INVALID, "null filter handle in set");
+        group_of[i] = uint32_t(fs[i]->device);
+    }
+    return PBF_OK;
+}
+
 int pbf_probe_multi_fixed(pbf_filter_t* const* filters, uint32_t nfilters, const uint8_t* keys, uint32_t key_len,
                           uint64_t n, uint8_t* const* hitmasks, int on_device) {
     if (key_len == 0 && n > 0) return fail(PBF_ERR_INVALID, "key_len 0: use pbf_probe_multi with offsets");
+    if (!on_device && filters && hitmasks && multi_device(filters, nfilters)) {
+        std::vector<uint32_t> grp;
+        int rc = by_device(filters, nfilters, grp);
+        if (rc) return rc;
+        return probe_multi_groups(filters, nfilters, grp.data(), keys, nullptr, key_len, n, hitmasks);
+    }
     return probe_multi_impl(filters, nfilters, keys, nullptr, key_len, n, hitmasks, on_device);
 }
 
 int pbf_probe_multi(pbf_filter_t* const* filters, uint32_t nfilters, const uint8_t* keys, const uint64_t* offsets,
                     uint64_t n, uint8_t* const* hitmasks, int on_device) {
     if (!offsets && n > 0) return fail(PBF_ERR_INVALID, "null offsets");
-    return probe_multi_impl(filters, nfilters, keys ? keys : reinterpret_cast<const uint8_t*>(offsets), offsets, 0, n,
-                            hitmasks, on_device);
+    const uint8_t* kp = keys ? keys : reinterpret_cast<const uint8_t*>(offsets);
+    if (!on_device && filters && hitmasks && multi_device(filters, nfilters)) {
+        std::vector<uint32_t> grp;
+        int rc = by_device(filters, nfilters, grp);
+        if (rc) return rc;
+        return probe_multi_groups(filters, nfilters, grp.data(), kp, offsets, 0, n, hitmasks);
+    }
+    return probe_multi_impl(filters, nfilters, kp, offsets, 0, n, hitmasks, on_device);
+}
+
+int pbf_probe_multi_placed(pbf_filter_t* const* filters, uint32_t nfilters, const uint32_t* group_of,
+                           const uint8_t* keys, const uint64_t* offsets, uint32_t key_len, uint64_t n,
+                           uint8_t* const* hitmasks) {
+    if (nfilters == 0) return PBF_OK;
+    if (!filters || !hitmasks || !group_of) return fail(PBF_ERR_INVALID, "null filter, group or hitmask array");
+    if (!offsets && key_len == 0 && n > 0) return fail(PBF_ERR_INVALID, "fixed keys need key_len > 0");
+    for (uint32_t i = 0; i < nfilters; ++i)
+        if (n && !hitmasks[i]) return fail(PBF_ERR_INVALID, "null hitmask in set");
+    const uint8_t* kp = keys ? keys : reinterpret_cast<const uint8_t*>(offsets);
+    return probe_multi_groups(filters, nfilters, group_of, kp, offsets, offsets ? 0 : key_len, n, hitmasks);
 }
 
 int pbf_hash_indices_fixed(pbf_filter_t* f, const uint8_t* keys, uint32_t key_len, uint64_t n, uint64_t* out,
@@ -2082,6 +2173,16 @@ int pbf_sync(pbf_filter_t* f) {
     int rc = enter(f);
     if (rc) return rc;
     return wait_stream(f);
+}
+
+int pbf_index_params(uint64_t nb_bytes, uint32_t* mode, uint64_t* magic, uint32_t* shift) {
+    if (!mode || !magic || !shift) return fail(PBF_ERR_INVALID, "null out");
+    if (nb_bytes == 0) return fail(PBF_ERR_ZERO_SIZE, "nb_bytes == 0 (integer modulo by zero)");
+    const IndexMap im = make_index_map(nb_bytes * 8);
+    *mode = im.mode;
+    *magic = im.magic;
+    *shift = im.mask;
+    return PBF_OK;
 }
 
 int pbf_wait_stream(pbf_filter_t* f, void* stream) {

@@ -367,3 +367,34 @@ def test_c5_geometry_small_sets_ragged_and_spills(oracle, nf):
     assert detail & _native.PBF_DETAIL_RING and (detail >> 8) & 0xFF == nf, hex(detail)
     b0 = np.unpackbits(got[0], bitorder="little")[:nq]
     assert b0[base:base + 60_000].all()  # the repeated member hits filter 0 every time
+
+
+def test_multi_placement_groups_one_thread_each(oracle):
+    """A filter set in placement groups (LsmStorage.get's filters placed one per GPU, probed from
+    one process: pbf_probe_multi_placed): each group runs on its own host thread and stages the
+    host batch to its device itself.  On the one-GPU box every group is on device 0 (the 8-GPU
+    shape is one group per device); masks come back in the set's (get) order and equal the
+    single-group probe and the oracle, for same-size filters (shared pipelines per group),
+    mixed sizes and variable-length keys."""
+    nb, k, n_per, count = 2 ** 21, 6, 60_000, 8
+    fs, want = _filters(oracle, nb, k, n_per, count)
+    small = BloomFilter(50_021, 7)
+    small_keys = PackedKeys.fixed(splitmix_hex_keys(SEED, 5, 3000))
+    small.add_many(small_keys)
+    fs.append(small)
+    want.append(oracle.build(50_021, 7, small_keys))
+    q = PackedKeys.fixed(splitmix_hex_keys(SEED, n_per // 3, count * n_per + 11))
+    groups = [i % 4 for i in range(len(fs))]
+    got = may_contain_multi(fs, q, groups=groups)
+    ref = may_contain_multi(fs, q)
+    assert np.array_equal(got, ref)
+    kk = [k] * count + [7]
+    for i in range(len(fs)):
+        assert np.array_equal(got[i], oracle.probe(want[i], kk[i], q)), i
+    d, o = varlen_keys(0xC3, 0, 20_000)
+    vq = PackedKeys(d, 20_000, offsets=o)
+    gv = may_contain_multi(fs, vq, groups=[3, 2, 1, 0, 3, 2, 1, 0, 5])
+    for i in range(len(fs)):
+        assert np.array_equal(gv[i], oracle.probe(want[i], kk[i], vq)), i
+    with pytest.raises(ValueError):
+        may_contain_multi([fs[0], fs[0]], q, groups=[0, 1])  # a filter twice

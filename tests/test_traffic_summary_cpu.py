@@ -21,6 +21,7 @@ def test_pass_of_names():
     assert pass_of("pbf::k_tile_build") == "build"
     assert pass_of("pbf::k_ovf_build") == "build"
     assert pass_of("pbf::k_tile_probe") == "probe"
+    assert pass_of("pbf::k_tile_probe_set<2>") == "probe"
     assert pass_of("pbf::k_gather_ring<1>") == "probe"
     assert pass_of("pbf::k_gather_ring<8>") == "probe"
     assert pass_of("pbf::k_hw_to_hitmask") == "probe"

@@ -29,7 +29,7 @@ traffic() {  # tag bench-args...: FETCH_SIZE and WRITE_SIZE in separate passes, 
   local tag=$1; shift
   run pmc_fetch_$tag 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_fetch_$tag -o run -- python bench.py --no-cpu-baseline --no-host-inclusive "$@"
   run pmc_write_$tag 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_write_$tag -o run -- python bench.py --no-cpu-baseline --no-host-inclusive "$@"
-  python tools/traffic_summary.py gpurun_out/pmc_fetch_$tag gpurun_out/pmc_write_$tag gpurun_out/traffic_$tag.json --config $tag > gpurun_out/traffic_${tag}_summary.txt 2>&1 || true
+  python tools/traffic_summary.py gpurun_out/pmc_fetch_$tag gpurun_out/pmc_write_$tag gpurun_out/traffic_$tag.json --config $tag ${TRAFFIC_ARGS:-} > gpurun_out/traffic_${tag}_summary.txt 2>&1 || true
 }
 abenv() {  # tag seconds rounds bench-args...: the default vs the environment in PBF_AB_ENV (VAR=value)
   local tag=$1 secs=$2 rounds=$3; shift 3
@@ -59,7 +59,9 @@ for step in "$@"; do
     prof) prof prof 600 --steps 20 --warmup 5 --no-cpu-baseline --no-host-inclusive ;;
     profq) prof profq 300 --steps 20 --warmup 5 --no-cpu-baseline --no-host-inclusive ;;
     traffic) traffic c2 --steps 5 --warmup 2 ;;
-    traffic_c3) traffic c3 --config c3 --steps 2 --warmup 1 ;;  # then re-run traffic_summary with --probe-scale 2.0 (two equal 100M-key pipelines)
+    traffic_c3) TRAFFIC_ARGS="--probe-scale 2.0" traffic c3 --config c3 --steps 2 --warmup 1 ;;  # two equal 100M-key pipelines per probe pass
+    traffic_c4) traffic c4 --config c4 --steps 2 --warmup 1 ;;  # per-filter build pass (bench scales by the rank's filters)
+    traffic_c5) TRAFFIC_ARGS="--probe-scale 3.0" traffic c5 --config c5 --steps 2 --warmup 1 --no-host-c5 ;;  # three equal pipelines
     pmcall) run pmcall 2400 tools/pmc_passes.sh gpurun_out/pmcall ;;
     pmc_c3) run pmc_c3 2400 tools/pmc_passes.sh gpurun_out/pmc_c3 --config c3 ;;
     pmc_c4) run pmc_c4 2400 tools/pmc_passes.sh gpurun_out/pmc_c4 --config c4 ;;

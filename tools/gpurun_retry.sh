@@ -2,7 +2,7 @@
 # gpurun with waits on transient pool failures (no box free, box lost while being prepared).
 # Usage: tools/gpurun_retry.sh 'remote command'   (log: /tmp/gpurun_last.log)
 cd "$(dirname "$0")/.."
-for attempt in 1 2 3 4 5 6; do
+for attempt in $(seq 1 ${GPURUN_ATTEMPTS:-20}); do
   rm -rf gpurun_out/*
   /usr/local/graft/bin/gpurun --timeout 1200 -- "$1" > /tmp/gpurun_last.log 2>&1
   rc=$?

@@ -53,7 +53,8 @@ def pass_of(kernel: str) -> str | None:
     if kernel.split("<")[0] in ("pbf::k_tile_build", "pbf::k_ovf_build"):
         return "build"
     # templated kernels (k_gather_ring<NF>) match on the name before the argument list
-    if kernel.split("<")[0] in ("pbf::k_tile_probe", "pbf::k_gather", "pbf::k_gather_ring", "pbf::k_hw_to_hitmask"):
+    if kernel.split("<")[0] in ("pbf::k_tile_probe", "pbf::k_tile_probe_set", "pbf::k_gather", "pbf::k_gather_ring",
+                                "pbf::k_hw_to_hitmask"):
         return "probe"
     return None
 
