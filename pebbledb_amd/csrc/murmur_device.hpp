@@ -112,6 +112,9 @@ __device__ __forceinline__ void murmur_seeds_seg(const uint8_t* p, uint32_t len,
     const uint32_t off = uint32_t(a & 15), w0 = off >> 2, sh = off & 3;
     const uint32_t nb = len >> 2, t = len & 3;
     const uint32_t nchunks = len ? (off + len + 15) >> 4 : 0;
+    // the tail's dwords are loaded up front, beside the first segment's chunks (its latency then
+    // overlaps the block rounds instead of following them)
+    const uint32_t tail = t ? load_tail(p + 4 * nb, t) : 0u;
     for (uint32_t seg = 0; seg * 16 < nb; ++seg) {
         uint32_t W[20];
 #pragma unroll
@@ -141,7 +144,7 @@ __device__ __forceinline__ void murmur_seeds_seg(const uint8_t* p, uint32_t len,
         }
     }
     if (t) {
-        const uint32_t km = mix_block(load_tail(p + 4 * nb, t));
+        const uint32_t km = mix_block(tail);
 #pragma unroll
         for (int s = 0; s < KMAX; ++s) h[s] ^= km;
     }

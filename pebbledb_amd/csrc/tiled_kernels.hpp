@@ -263,14 +263,24 @@ __global__ void __launch_bounds__(kPartThreads) k_part(KeySet ks, uint64_t n, in
         }
         __syncthreads();  // before any spill of this workgroup ORs into neg
     }
-    // fixed 16-byte keys: a sub-chunk's keys are loaded one sub-chunk ahead
+    // fixed 16-byte keys: a sub-chunk's keys are loaded one sub-chunk ahead; variable-length keys:
+    // their byte offsets are (the key bytes then need one dependent load, not two)
     uint4 kw[KM == kFixed16 ? KPT : 1];
+    uint64_t koa[KM == kVar ? KPT : 1], kob[KM == kVar ? KPT : 1];
+    const uint64_t kvo0 = KM == kVar ? gld(ks.off0) : 0;
     auto load_keys = [&](uint64_t s0) {
         if constexpr (KM == kFixed16) {
 #pragma unroll
             for (int u = 0; u < KPT; ++u) {
                 const uint64_t i = min(s0 + u * nt + tid, n - 1);
                 kw[u] = ld_stream_nt<kNtKeys>(reinterpret_cast<const uint32_t*>(ks.data) + i * 4);
+            }
+        } else if constexpr (KM == kVar) {
+#pragma unroll
+            for (int u = 0; u < KPT; ++u) {
+                const uint64_t i = min(s0 + u * nt + tid, n - 1);
+                koa[u] = gld(ks.offsets + i);
+                kob[u] = gld(ks.offsets + i + 1);
             }
         }
     };
@@ -292,6 +302,8 @@ __global__ void __launch_bounds__(kPartThreads) k_part(KeySet ks, uint64_t n, in
             if (uint32_t(u) < kpt && i < s1) {
                 if constexpr (KM == kFixed16)
                     murmur_seeds16<KMAX>(kw[u], k, emit);
+                else if constexpr (KM == kVar && KMAX > 0)
+                    murmur_seeds_seg<KMAX>(ks.data + (koa[u] - kvo0), uint32_t(kob[u] - koa[u]), k, emit);
                 else
                     hash_key<KMAX, KM>(ks, i, k, emit);
             }
@@ -516,27 +528,49 @@ __global__ void __launch_bounds__(1024) k_tile_build(TileMap tm, PartGeom pg, co
     const uint32_t lane = tid & 63, wave = tid >> 6, nwaves = nt >> 6;
     const uint32_t lmask = (1u << tm.tb) - 1u;
     constexpr int U = kTileBuildRegionsInFlight;
-    for (uint32_t g0 = wave; g0 < G; g0 += nwaves * U) {
-        uint4 v[U];
-        uint32_t f[U];
+    if (cap <= 256) {
+        // every region fits one 256-entry chunk (C2: ~230 entries): U regions in flight per wave
+        for (uint32_t g0 = wave; g0 < G; g0 += nwaves * U) {
+            uint4 v[U];
+            uint32_t f[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint32_t q = g0 + u * nwaves;
-            f[u] = q < G ? fills[q] : 0u;
-            // unconditional loads, clamped to the filled part (idle lanes re-read its last line)
-            const uint32_t lc = min(lane, (max(f[u], 1u) - 1) >> 2);
-            v[u] = ld_stream_nt<kNtLoad>(regions + region_id(min(q, G - 1), b, G, B) * cap + lc * 4);
+            for (int u = 0; u < U; ++u) {
+                const uint32_t q = g0 + u * nwaves;
+                f[u] = q < G ? fills[q] : 0u;
+                // unconditional loads, clamped to the filled part (idle lanes re-read its last line)
+                const uint32_t lc = min(lane, (max(f[u], 1u) - 1) >> 2);
+                v[u] = ld_stream_nt<kNtLoad>(regions + region_id(min(q, G - 1), b, G, B) * cap + lc * 4);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (lane * 4 < f[u]) or_bits4(tile, v[u], lane * 4, f[u], lmask);
         }
+    } else {
+        // regions of many chunks (C4: ~2,850 entries, C3: ~760): the wave walks the (region,
+        // chunk) sequence of its regions with U chunks in flight — one region's chunk after
+        // another, so a long region does not leave the wave with one load in flight at a time.
+        // The walk is wave-uniform (fills are in LDS).
+        uint32_t q = wave, c = 0;  // next chunk to issue: region q, entries [256c, 256c + 256)
+        while (q < G) {
+            uint4 v[U];
+            uint32_t f[U], e[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u)
-            if (lane * 4 < f[u]) or_bits4(tile, v[u], lane * 4, f[u], lmask);
-    }
-    // regions holding more than 256 entries
-    if (cap > 256) {
-        for (uint32_t q = wave; q < G; q += nwaves) {
-            const uint32_t fq = fills[q];
-            for (uint32_t c = 64 + lane; c * 4 < fq; c += 64)
-                or_bits4(tile, ld_stream_nt<kNtLoad>(regions + region_id(q, b, G, B) * cap + c * 4), c * 4, fq, lmask);
+            for (int u = 0; u < U; ++u) {
+                while (q < G && c * 256 >= fills[q]) {
+                    q += nwaves;
+                    c = 0;
+                }
+                const bool live = q < G;
+                f[u] = live ? fills[q] : 0u;
+                e[u] = c * 256 + lane * 4;
+                const uint32_t qq = live ? q : G - 1, fq = live ? f[u] : 1u;
+                const uint32_t ec = min(e[u], (fq - 1) & ~3u);  // clamped: idle lanes re-read a filled line
+                v[u] = ld_stream_nt<kNtLoad>(regions + region_id(qq, b, G, B) * cap + ec);
+                if (live) ++c;
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (e[u] < f[u]) or_bits4(tile, v[u], e[u], f[u], lmask);
         }
     }
     lds_barrier();
