@@ -81,6 +81,7 @@ for step in "$@"; do
     prof_c4) prof prof_c4 600 --config c4 --steps 2 --warmup 1 --no-cpu-baseline ;;
     prof_c5) prof prof_c5 600 --config c5 --steps 3 --warmup 1 --no-cpu-baseline --no-host-c5 ;;
     ab) ab ab 300 2 --steps 50 --warmup 5 ;;
+    unaligned) run unaligned 120 tools/microbench/unaligned_loads ;;
     parity_var) for v in build/variants/*.so; do
                   nm=$(basename $v .so)
                   PBF_LIB=$PWD/$v run parity_$nm 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_multi.py tests/test_gpu_lsm_get.py tests/test_gpu_device_resident.py -m gpu -x -q -rf --timeout 150 --timeout-method thread -k "${PBF_PARITY_K:-not config4 and not config3}"
