@@ -252,6 +252,18 @@ int pbf_build_sstables(pbf_filter_t* const* filters, uint32_t ntables, const uin
 int pbf_plan_blocks(const uint64_t* key_offsets, const uint64_t* value_offsets, uint64_t n, uint64_t block_size,
                     uint64_t* block_first, uint64_t* block_out, uint64_t* nblocks);
 
+/* Compaction's output split (LsmStorage._compact, src/lsm_storage.py:233-251) over n records,
+ * host-side: the greedy blocks of pbf_plan_blocks over the whole run, a new table whenever the
+ * builder's position (advanced per finished block, src/sstable.py:246-266) reaches
+ * max_sstable_size (the table's last block then holds only the record that finished the previous
+ * one), the last builder kept only if its position is past 0.  Outputs for pbf_build_sstables:
+ * block_first / block_out (n+1 entries each; block_out laid end to end over the tables' data
+ * sections), table_blocks (n+1 entries; table t = blocks [table_blocks[t], table_blocks[t+1])),
+ * the counts, and the records covered (*written <= n). */
+int pbf_plan_compaction(const uint64_t* key_offsets, const uint64_t* value_offsets, uint64_t n, uint64_t block_size,
+                        uint64_t max_sstable_size, uint64_t* block_first, uint64_t* block_out, uint64_t* table_blocks,
+                        uint64_t* nblocks, uint64_t* ntables, uint64_t* written);
+
 /* The level key-range pre-check of LsmStorage.get (src/lsm_storage.py:171-175) for a batch:
  * out[t * ceil(n/8) + i/8] bit (i & 7) = (first_t <= key_i <= last_t), Python str order =
  * bytewise lexicographic order of the UTF-8 keys.  Bounds are 2*ntables byte strings

@@ -67,6 +67,8 @@ SIGNATURES = {
     "pbf_encode_data_blocks": (_int, [_int, _u8p, _vp, _u8p, _vp, _u64, _vp, _vp, _u64, _u8p, _int]),
     "pbf_build_sstable": (_int, [_vp, _u8p, _vp, _u8p, _vp, _u64, _vp, _vp, _u64, _u8p, _u8p]),
     "pbf_build_sstables": (_int, [_vp, _u32, _u8p, _vp, _u8p, _vp, _u64, _vp, _vp, _u64, _vp, _vp, _vp]),
+    "pbf_plan_compaction": (_int, [_vp, _vp, _u64, _u64, _u64, _vp, _vp, _vp, ctypes.POINTER(_u64), ctypes.POINTER(_u64),
+                                   ctypes.POINTER(_u64)]),
     "pbf_plan_blocks": (_int, [_vp, _vp, _u64, _u64, _vp, _vp, ctypes.POINTER(_u64)]),
     "pbf_key_range_mask": (_int, [_int, _vp, _u8p, _vp, _u32, _u64, _u8p, _vp, _u32, _u8p, _int]),
     "pbf_gen_splitmix_hex": (_int, [_int, _vp, _u8p, _u64, _u64, _u64]),

@@ -238,7 +238,7 @@ namespace {
 // one for the duration of its host-side enqueue, and the GPU-side reuse across streams is
 // ordered by the set's `last` event (the next user's stream waits on it).
 struct Scratch {
-    DevBuf regions, fill, ovf, ovf_count, pref, rbits, neg, hw;
+    DevBuf regions, fill, ovf, ovf_count, pref, rbits, neg, hw, perm;
     uint32_t ovf_phase = 0;  // which of the two overflow counters the next build uses
     bool ovf_init = false;
     DevBuf dkeys, doffs, dout;
@@ -249,7 +249,7 @@ struct Scratch {
     hipStream_t last_stream = nullptr;  // ... on this stream
     bool leased = false;
     void release_all() {
-        for (DevBuf* d : {&regions, &fill, &ovf, &ovf_count, &pref, &rbits, &neg, &hw, &dkeys, &doffs, &dout,
+        for (DevBuf* d : {&regions, &fill, &ovf, &ovf_count, &pref, &rbits, &neg, &hw, &perm, &dkeys, &doffs, &dout,
                           &svals, &splan, &ssec, &serr})
             d->release();
         pin[0].release();
@@ -547,6 +547,7 @@ Batch make_batch(const uint8_t* keys, const uint64_t* offsets, uint32_t key_len,
     b.ks.offsets = offsets;
     b.ks.off0 = offsets;
     b.ks.key_len = key_len;
+    b.ks.perm = nullptr;
     b.n = n;
     if (offsets)
         b.km = kVar;
@@ -781,6 +782,24 @@ void with_part_kernel(uint32_t k, L&& launch) {
     launch(k_part<KX, KMD, PROBE>);
 }
 
+// Variable-length keys through the counting-sort partition: rank each sub-chunk's keys by length
+// first (k_len_rank; PBF_LEN_RANK=0 turns it off for A/B measurements), so a partition wave
+// hashes keys of about one length.  Returns the key set the partition reads.
+int len_ranked(pbf_filter_t* f, const Batch& b, const PartGeom& pg, KeySet* out) {
+    static const bool on = [] {
+        const char* e = std::getenv("PBF_LEN_RANK");
+        return !(e && e[0] == '0');
+    }();
+    *out = b.ks;
+    if (b.km != kVar || pg.ring || !on || b.n == 0 || pg.kps > 4096) return PBF_OK;
+    HIP_TRY(f->sc->perm.ensure(size_t(b.n) * 2 + 16));
+    auto* perm = static_cast<uint16_t*>(f->sc->perm.p);
+    k_len_rank<<<uint32_t((b.n + pg.kps - 1) / pg.kps), 256, 0, f->stream>>>(b.ks, b.n, pg.kps, perm);
+    LAUNCHED(f, "k_len_rank");
+    out->perm = perm;
+    return PBF_OK;
+}
+
 int run_tiled(pbf_filter_t* f, const Batch& b) {
     const TileMap& tm = f->tm;
     const uint32_t B = tm.nbuckets;
@@ -802,6 +821,9 @@ int run_tiled(pbf_filter_t* f, const Batch& b) {
     uint32_t* ovf_next = static_cast<uint32_t*>(f->sc->ovf_count.p) + (f->sc->ovf_phase ^ 1);
     f->sc->ovf_phase ^= 1;
     hipStream_t s = f->stream;
+    KeySet pks{};
+    int rrc = len_ranked(f, b, pg, &pks);
+    if (rrc) return rrc;
     hipError_t err = hipSuccess;
     dispatch(kmax_for(k), b.km, [&](auto KMAX, auto KM) {
         if constexpr (decltype(KMAX)::value > 0) {  // tiled path only for k <= 32
@@ -819,7 +841,7 @@ int run_tiled(pbf_filter_t* f, const Batch& b) {
                 with_part_kernel<KX, KMD, false>(k, [&](auto kern) {
                     err = allow_lds(kern, pl.lds_part);
                     if (err == hipSuccess)
-                        kern<<<pg.G, kPartThreads, pl.lds_part, s>>>(b.ks, b.n, int(k), tm, pg, regions, fill, nullptr,
+                        kern<<<pg.G, kPartThreads, pl.lds_part, s>>>(pks, b.n, int(k), tm, pg, regions, fill, nullptr,
                                                              ovf, ovf_count, ProbeSet{}, nullptr);
                 });
             }
@@ -891,6 +913,9 @@ int run_tiled_probe_set(pbf_filter_t* f, pbf_filter_t* const* fs, uint32_t nf, c
     auto tprobe_set = tab == 2 ? k_tile_probe_set<2> : (tab == 1 ? k_tile_probe_set<1> : k_tile_probe_set<0>);
     HIP_TRY(allow_lds(tprobe, lds_tile));
     // the partition zeroes neg (and presets hw for the gather) itself
+    KeySet pks{};
+    int rrc = len_ranked(f, b, pg, &pks);
+    if (rrc) return rrc;
     hipError_t err = hipSuccess;
     dispatch(kmax_for(k), b.km, [&](auto KMAX, auto KM) {
         if constexpr (decltype(KMAX)::value > 0) {
@@ -908,7 +933,7 @@ int run_tiled_probe_set(pbf_filter_t* f, pbf_filter_t* const* fs, uint32_t nf, c
                 with_part_kernel<KX, KMD, true>(k, [&](auto kern) {
                     err = allow_lds(kern, pl.lds_part);
                     if (err == hipSuccess)
-                        kern<<<pg.G, kPartThreads, pl.lds_part, s>>>(b.ks, b.n, int(k), tm, pg, regions, fill, pref,
+                        kern<<<pg.G, kPartThreads, pl.lds_part, s>>>(pks, b.n, int(k), tm, pg, regions, fill, pref,
                                                              nullptr, nullptr, ps, use_hw ? hw : nullptr);
                 });
             }
@@ -1986,7 +2011,7 @@ int pbf_scratch_bytes(int device, uint64_t* out) {
     std::lock_guard<std::mutex> lock(pool.mu);
     uint64_t t = 0;
     for (Scratch* sc : pool.sets)
-        for (const DevBuf* d : {&sc->regions, &sc->fill, &sc->ovf, &sc->ovf_count, &sc->pref, &sc->rbits, &sc->neg, &sc->hw, &sc->dkeys, &sc->doffs, &sc->dout, &sc->svals, &sc->splan,
+        for (const DevBuf* d : {&sc->regions, &sc->fill, &sc->ovf, &sc->ovf_count, &sc->pref, &sc->rbits, &sc->neg, &sc->hw, &sc->perm, &sc->dkeys, &sc->doffs, &sc->dout, &sc->svals, &sc->splan,
                                 &sc->ssec, &sc->serr})
             t += d->bytes;
     *out = t;
@@ -2642,6 +2667,67 @@ int pbf_plan_blocks(const uint64_t* key_offsets, const uint64_t* value_offsets, 
     block_first[nb] = n;
     block_out[nb] = out;
     *nblocks = nb;
+    return PBF_OK;
+}
+
+int pbf_plan_compaction(const uint64_t* key_offsets, const uint64_t* value_offsets, uint64_t n, uint64_t block_size,
+                        uint64_t max_sstable_size, uint64_t* block_first, uint64_t* block_out, uint64_t* table_blocks,
+                        uint64_t* nblocks, uint64_t* ntables, uint64_t* written) {
+    if (!key_offsets || !value_offsets || !block_first || !block_out || !table_blocks || !nblocks || !ntables || !written)
+        return fail(PBF_ERR_INVALID, "null pointer");
+    if (block_size == 0 || block_size > kMaxBlockData) return fail(PBF_ERR_INVALID, "block_size must be in (0, 65536]");
+    // LsmStorage._compact (lsm_storage.py:233-251) over the greedy blocks of DataBlockBuilder.add
+    // (blocks.py:78-95): a builder's position advances when a record does not fit the open block
+    // (sstable.py:246-266); at position >= max_sstable_size the builder is built, its last block
+    // holding only that record; at the end the last builder is built only if its position is > 0
+    uint64_t nb = 0, nt = 0, out = 0;  // blocks, tables, byte offset (outputs' data end to end)
+    block_first[0] = 0;
+    block_out[0] = 0;
+    table_blocks[0] = 0;
+    uint64_t i = 0;
+    while (i < n) {
+        uint64_t pos = 0, used = 0, cnt = 0;  // builder position; the open block's bytes / records
+        bool split = false;
+        const uint64_t nb_table0 = nb;
+        for (; i < n; ++i) {
+            const uint64_t sz = (key_offsets[i + 1] - key_offsets[i]) + (value_offsets[i + 1] - value_offsets[i]) + 8;
+            if (sz > block_size) return fail(PBF_ERR_INVALID, "a record is larger than block_size");
+            if (cnt && used + sz > block_size) {  // record i finishes the open block
+                const uint64_t bsz = used + 2 * cnt + 2;
+                pos += bsz;
+                out += bsz;
+                block_first[++nb] = i;
+                block_out[nb] = out;
+                used = 0;
+                cnt = 0;
+                if (pos >= max_sstable_size) {  // build(): [i] alone is the table's last block
+                    out += sz + 4;
+                    block_first[++nb] = i + 1;
+                    block_out[nb] = out;
+                    table_blocks[++nt] = nb;
+                    ++i;
+                    split = true;
+                    break;
+                }
+            }
+            used += sz;
+            ++cnt;
+        }
+        if (!split) {
+            if (pos > 0) {  // the open block ends the last table
+                out += used + 2 * cnt + 2;
+                block_first[++nb] = n;
+                block_out[nb] = out;
+                table_blocks[++nt] = nb;
+            } else {  // records of the last builder's first open block are not written
+                nb = nb_table0;
+            }
+            break;
+        }
+    }
+    *nblocks = nb;
+    *ntables = nt;
+    *written = block_first[nb];
     return PBF_OK;
 }
 

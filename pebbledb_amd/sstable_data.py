@@ -157,6 +157,30 @@ def plan_compaction(ko: np.ndarray, vo: np.ndarray, block_size: int = BLOCK_SIZE
     return bf, bo, tb, int(bf[-1])
 
 
+def plan_compaction_native(ko: np.ndarray, vo: np.ndarray, block_size: int = BLOCK_SIZE,
+                           max_sstable_size: int = 262_144_000):
+    """plan_compaction by the C planner (pbf_plan_compaction: one pass over the record sizes)."""
+    n = len(ko) - 1
+    if not 0 < block_size <= 65_536:
+        raise ValueError("block_size must be in (0, 65536]: DataBlock offsets are u16 (blocks.py:34)")
+    if n <= 0:
+        return (np.zeros(1, np.uint64), np.zeros(1, np.uint64), np.zeros(1, np.uint64), 0)
+    ko = np.ascontiguousarray(ko, dtype=np.uint64)
+    vo = np.ascontiguousarray(vo, dtype=np.uint64)
+    bf = np.empty(n + 1, dtype=np.uint64)
+    bo = np.empty(n + 1, dtype=np.uint64)
+    tb = np.empty(n + 1, dtype=np.uint64)
+    nb, nt, w = ctypes.c_uint64(0), ctypes.c_uint64(0), ctypes.c_uint64(0)
+    vp = ctypes.c_void_p
+    rc = _native.lib().pbf_plan_compaction(vp(ko.ctypes.data), vp(vo.ctypes.data), n, block_size, max_sstable_size,
+                                           vp(bf.ctypes.data), vp(bo.ctypes.data), vp(tb.ctypes.data), ctypes.byref(nb),
+                                           ctypes.byref(nt), ctypes.byref(w))
+    if rc == _native.PBF_ERR_INVALID and "larger than block_size" in _native.lib().pbf_last_error().decode():
+        raise ValueError("a record is larger than block_size (the reference would drop it, blocks.py:84-85)")
+    _native.check(rc, "pbf_plan_compaction")
+    return bf[:nb.value + 1].copy(), bo[:nb.value + 1].copy(), tb[:nt.value + 1].copy(), int(w.value)
+
+
 def encode_data_blocks(pk: PackedKeys, vals: np.ndarray, vo: np.ndarray, block_first: np.ndarray,
                        block_out: np.ndarray, device: int = 0) -> np.ndarray:
     """The data section (every encoded DataBlock back to back), written by the device."""
@@ -275,7 +299,7 @@ def build_sstables(keys, values=None, max_sstable_size: int = 262_144_000, block
         raise ValueError("keys and values differ in length")
     ko = np.ascontiguousarray(key_offsets(pk), dtype=np.uint64)
     vo = np.ascontiguousarray(vo, dtype=np.uint64)
-    bf, bo, tb, written = plan_compaction(ko, vo, block_size, max_sstable_size)
+    bf, bo, tb, written = plan_compaction_native(ko, vo, block_size, max_sstable_size)
     nt = len(tb) - 1
     if nt == 0:
         return [], written

@@ -65,3 +65,40 @@ def test_plan_empty_and_oversized_records():
     ko = np.array([0, 2000], np.uint64)
     with pytest.raises(ValueError):
         plan_compaction(ko, np.zeros(2, np.uint64), 1024, 4096)
+
+
+@pytest.mark.parametrize("case", CASES, ids=[c["name"] for c in CASES])
+def test_native_planner_equals_restatement(case):
+    """pbf_plan_compaction (C, what build_sstables uses) == plan_compaction (numpy) on the golden
+    runs and on random runs with many split points (host-side, no GPU)."""
+    from pebbledb_amd.sstable_data import plan_compaction_native
+    keys, vals = case_records(case)
+    pk = PackedKeys.from_strs(keys)
+    _, vo = pack_values(vals)
+    ko = np.asarray(key_offsets(pk), np.uint64)
+    a = plan_compaction(ko, vo, case["block_size"], case["max_sstable_size"])
+    b = plan_compaction_native(ko, vo, case["block_size"], case["max_sstable_size"])
+    for x, y in zip(a[:3], b[:3]):
+        assert np.array_equal(x, y)
+    assert a[3] == b[3]
+
+
+def test_native_planner_random_runs():
+    from pebbledb_amd.sstable_data import plan_compaction_native
+    rng = np.random.default_rng(3)
+    for trial in range(40):
+        n = int(rng.integers(1, 3000))
+        bs = int(rng.choice([64, 256, 1000, 4096]))
+        kl = rng.integers(0, 24, n)
+        vl = rng.integers(0, max(1, bs - 8 - 24), n)
+        vl = np.minimum(vl, bs - 8 - kl)
+        ko = np.zeros(n + 1, np.uint64)
+        vo = np.zeros(n + 1, np.uint64)
+        np.cumsum(kl, out=ko[1:])
+        np.cumsum(vl, out=vo[1:])
+        mx = int(rng.integers(1, 20 * bs))
+        a = plan_compaction(ko, vo, bs, mx)
+        b = plan_compaction_native(ko, vo, bs, mx)
+        for x, y in zip(a[:3], b[:3]):
+            assert np.array_equal(x, y), trial
+        assert a[3] == b[3], trial
