@@ -182,11 +182,6 @@ IndexMap make_index_map(uint64_t m) {
     if (pow2 && m <= (uint64_t(1) << 32)) {
         im.mode = kPow2;
         im.mask = uint32_t(m - 1);
-#ifdef PBF_AB_LEMIRE_INDEX
-    } else if (m < (uint64_t(1) << 31)) {
-        im.mode = kSmall;
-        im.magic = ~uint64_t(0) / m + 1;
-#endif
     } else if (m < (uint64_t(1) << 30)) {
         // mod_small's reciprocal: l = ceil(log2 m), M = ceil(2^(31+l) / m) < 2^32, shift l-1
         uint32_t l = 0;
