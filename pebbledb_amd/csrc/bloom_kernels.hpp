@@ -30,7 +30,6 @@ struct KeySet {
     const uint64_t* offsets;  // kVar only: offsets of this batch's keys
     const uint64_t* off0;     // kVar only: offsets[] value that maps to data[0]
     uint32_t key_len;         // kFixed*
-    const uint16_t* perm;     // kVar, counting-sort partition only (k_len_rank): the sub-chunk's keys by length
 };
 
 // Hash key i with seeds sbase..sbase+k-1 and call emit(s, hash_u32), s = 0..k-1.

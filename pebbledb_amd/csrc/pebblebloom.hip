@@ -116,7 +116,10 @@ size_t stage_bytes() {
     }();
     return v;
 }
-constexpr uint64_t kMaxPositions = uint64_t(1) << 30; // tiled pipeline batch (4 GiB of positions)
+// Positions per tiled pipeline: the partition counts them in u32 (fill, overflow list).  Round 3
+// capped pipelines at 2^30 positions: C4's 125M-key filters (1.25G positions) ran as 107M + 18M
+// keys, and the second pipeline's tile pass streamed the whole 225 MB bitmap again for 18M keys.
+constexpr uint64_t kMaxPositions = (uint64_t(1) << 32) - (uint64_t(1) << 26);
 
 // Words loaded in the direct probe's first stage (k_probe): 2 measured best of 1/2/6
 // (profiles/r02/s1, the direct probe is the small-batch path).
@@ -233,7 +236,7 @@ namespace {
 // one for the duration of its host-side enqueue, and the GPU-side reuse across streams is
 // ordered by the set's `last` event (the next user's stream waits on it).
 struct Scratch {
-    DevBuf regions, fill, ovf, ovf_count, pref, rbits, neg, hw, perm;
+    DevBuf regions, fill, ovf, ovf_count, pref, rbits, neg, hw;
     uint32_t ovf_phase = 0;  // which of the two overflow counters the next build uses
     bool ovf_init = false;
     DevBuf dkeys, doffs, dout;
@@ -244,7 +247,7 @@ struct Scratch {
     hipStream_t last_stream = nullptr;  // ... on this stream
     bool leased = false;
     void release_all() {
-        for (DevBuf* d : {&regions, &fill, &ovf, &ovf_count, &pref, &rbits, &neg, &hw, &perm, &dkeys, &doffs, &dout,
+        for (DevBuf* d : {&regions, &fill, &ovf, &ovf_count, &pref, &rbits, &neg, &hw, &dkeys, &doffs, &dout,
                           &svals, &splan, &ssec, &serr})
             d->release();
         pin[0].release();
@@ -542,7 +545,6 @@ Batch make_batch(const uint8_t* keys, const uint64_t* offsets, uint32_t key_len,
     b.ks.offsets = offsets;
     b.ks.off0 = offsets;
     b.ks.key_len = key_len;
-    b.ks.perm = nullptr;
     b.n = n;
     if (offsets)
         b.km = kVar;
@@ -777,24 +779,6 @@ void with_part_kernel(uint32_t k, L&& launch) {
     launch(k_part<KX, KMD, PROBE>);
 }
 
-// Variable-length keys through the counting-sort partition: rank each sub-chunk's keys by length
-// first (k_len_rank; PBF_LEN_RANK=0 turns it off for A/B measurements), so a partition wave
-// hashes keys of about one length.  Returns the key set the partition reads.
-int len_ranked(pbf_filter_t* f, const Batch& b, const PartGeom& pg, KeySet* out) {
-    static const bool on = [] {
-        const char* e = std::getenv("PBF_LEN_RANK");
-        return !(e && e[0] == '0');
-    }();
-    *out = b.ks;
-    if (b.km != kVar || pg.ring || !on || b.n == 0 || pg.kps > 4096) return PBF_OK;
-    HIP_TRY(f->sc->perm.ensure(size_t(b.n) * 2 + 16));
-    auto* perm = static_cast<uint16_t*>(f->sc->perm.p);
-    k_len_rank<<<uint32_t((b.n + pg.kps - 1) / pg.kps), 256, 0, f->stream>>>(b.ks, b.n, pg.kps, perm);
-    LAUNCHED(f, "k_len_rank");
-    out->perm = perm;
-    return PBF_OK;
-}
-
 int run_tiled(pbf_filter_t* f, const Batch& b) {
     const TileMap& tm = f->tm;
     const uint32_t B = tm.nbuckets;
@@ -816,9 +800,7 @@ int run_tiled(pbf_filter_t* f, const Batch& b) {
     uint32_t* ovf_next = static_cast<uint32_t*>(f->sc->ovf_count.p) + (f->sc->ovf_phase ^ 1);
     f->sc->ovf_phase ^= 1;
     hipStream_t s = f->stream;
-    KeySet pks{};
-    int rrc = len_ranked(f, b, pg, &pks);
-    if (rrc) return rrc;
+    const KeySet pks = b.ks;
     hipError_t err = hipSuccess;
     dispatch(kmax_for(k), b.km, [&](auto KMAX, auto KM) {
         if constexpr (decltype(KMAX)::value > 0) {  // tiled path only for k <= 32
@@ -908,9 +890,7 @@ int run_tiled_probe_set(pbf_filter_t* f, pbf_filter_t* const* fs, uint32_t nf, c
     auto tprobe_set = tab == 2 ? k_tile_probe_set<2> : (tab == 1 ? k_tile_probe_set<1> : k_tile_probe_set<0>);
     HIP_TRY(allow_lds(tprobe, lds_tile));
     // the partition zeroes neg (and presets hw for the gather) itself
-    KeySet pks{};
-    int rrc = len_ranked(f, b, pg, &pks);
-    if (rrc) return rrc;
+    const KeySet pks = b.ks;
     hipError_t err = hipSuccess;
     dispatch(kmax_for(k), b.km, [&](auto KMAX, auto KM) {
         if constexpr (decltype(KMAX)::value > 0) {
@@ -1008,7 +988,9 @@ uint64_t tiled_probe_batch(pbf_filter_t* f, int km, uint32_t nf, uint64_t total)
     const uint32_t k = f->k;
     auto fits = [&](uint64_t m) {
         const PartPlan pl = plan_for(f->tm, k, km, m, true, nf);
-        return pl.lds_gather <= 156 * 1024 && pl.pg.cap <= 65535;
+        // the tile test addresses a region word by a u32 global index (run_tiled_probe_set)
+        return pl.lds_gather <= 156 * 1024 && pl.pg.cap <= 65535 &&
+               uint64_t(pl.pg.G) * f->tm.nbuckets * (pl.pg.cap / 32) < (uint64_t(1) << 32);
     };
     const uint64_t top = std::max<uint64_t>(64, (kMaxPositions / k) & ~uint64_t(63));
     uint64_t n = top;
@@ -1032,8 +1014,11 @@ uint64_t tiled_probe_batch(pbf_filter_t* f, int km, uint32_t nf, uint64_t total)
 int add_device(pbf_filter_t* f, const Batch& b) {
     if (b.n == 0 || f->k == 0) return PBF_OK;
     if (want_tiled(f, b.n)) {
-        // positions are indexed by u32 inside one pipeline: batch very large inputs
-        const uint64_t per = std::max<uint64_t>(1, kMaxPositions / f->k);
+        // positions are counted in u32 inside one pipeline, and a region holds < 2^24 entries
+        // (the partitions' 24-bit region addressing): batch very large inputs
+        const double share = busiest_tile_share(f->tm);
+        const double cap_keys = double((1u << 24) - 64) * part_max_groups(false) / (double(f->k) * share * 1.25);
+        const uint64_t per = std::max<uint64_t>(1, std::min<uint64_t>(kMaxPositions / f->k, uint64_t(cap_keys)));
         for (uint64_t i0 = 0; i0 < b.n; i0 += per) {
             int rc = run_tiled(f, slice(b, i0, std::min<uint64_t>(per, b.n - i0)));
             if (rc) return rc;
@@ -2006,7 +1991,7 @@ int pbf_scratch_bytes(int device, uint64_t* out) {
     std::lock_guard<std::mutex> lock(pool.mu);
     uint64_t t = 0;
     for (Scratch* sc : pool.sets)
-        for (const DevBuf* d : {&sc->regions, &sc->fill, &sc->ovf, &sc->ovf_count, &sc->pref, &sc->rbits, &sc->neg, &sc->hw, &sc->perm, &sc->dkeys, &sc->doffs, &sc->dout, &sc->svals, &sc->splan,
+        for (const DevBuf* d : {&sc->regions, &sc->fill, &sc->ovf, &sc->ovf_count, &sc->pref, &sc->rbits, &sc->neg, &sc->hw, &sc->dkeys, &sc->doffs, &sc->dout, &sc->svals, &sc->splan,
                                 &sc->ssec, &sc->serr})
             t += d->bytes;
     *out = t;

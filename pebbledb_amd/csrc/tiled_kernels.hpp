@@ -199,52 +199,6 @@ __device__ __forceinline__ uint32_t bucket_of(const uint32_t* a, uint32_t B, uin
     return lo;
 }
 
-// ------------------------------------------------------------------ length ranking
-// Variable-length keys are hashed one per lane, and a wave runs the block rounds of its LONGEST
-// key (C3: 8-64-byte keys, 16 blocks executed for a mean of ~9).  One workgroup per partition
-// sub-chunk of kps keys (sub-chunks start at multiples of kps: a partition workgroup's key range
-// is a multiple of kps) writes perm[s0 + r] = the sub-chunk-local index of the key of rank r in
-// the order of block counts (len >> 2, capped at 63; ties in any order), so the partition's
-// thread slot r hashes that key and each of its waves holds keys of about one length.  Any
-// permutation gives the same bitmap / hit mask: an entry records its key's own index.
-__global__ void __launch_bounds__(256) k_len_rank(KeySet ks, uint64_t n, uint32_t kps, uint16_t* __restrict__ perm) {
-    __shared__ uint32_t cnt[64];
-    const uint32_t tid = threadIdx.x;
-    const uint64_t s0 = uint64_t(blockIdx.x) * kps;
-    const uint32_t m = uint32_t(min<uint64_t>(kps, n - s0));
-    if (tid < 64) cnt[tid] = 0;
-    __syncthreads();
-    constexpr int KPT = 16;  // kps <= 4096 = 16 x 256
-    uint32_t bk[KPT];
-#pragma unroll
-    for (int u = 0; u < KPT; ++u) {
-        const uint32_t t = u * 256 + tid;
-        bk[u] = 0;
-        if (t < m) {
-            const uint64_t a = gld(ks.offsets + s0 + t), b = gld(ks.offsets + s0 + t + 1);
-            bk[u] = min<uint64_t>((b - a) >> 2, 63);
-            atomicAdd(cnt + bk[u], 1u);
-        }
-    }
-    __syncthreads();
-    if (tid < 64) {  // exclusive scan of the 64 counts (one wave)
-        const uint32_t c = cnt[tid];
-        uint32_t v = c;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t o = __shfl_up(v, d, 64);
-            if (tid >= uint32_t(d)) v += o;
-        }
-        cnt[tid] = v - c;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int u = 0; u < KPT; ++u) {
-        const uint32_t t = u * 256 + tid;
-        if (t < m) perm[s0 + atomicAdd(cnt + bk[u], 1u)] = uint16_t(t);
-    }
-}
-
 // ------------------------------------------------------------------ partition
 // One 1024-thread workgroup per CU.  Each thread keeps up to KPT keys' KMAX (position, rank)
 // pairs in registers between the counting pass and the LDS placement, so every key is hashed
@@ -313,9 +267,6 @@ __global__ void __launch_bounds__(kPartThreads) k_part(KeySet ks, uint64_t n, in
     // their byte offsets are (the key bytes then need one dependent load, not two)
     uint4 kw[KM == kFixed16 ? KPT : 1];
     uint64_t koa[KM == kVar ? KPT : 1], kob[KM == kVar ? KPT : 1];
-    // kpj: the prefetched keys' sub-chunk-local indices; kj: those of the sub-chunk hashed last
-    // (its entries are placed one phase later)
-    uint32_t kpj[KM == kVar ? KPT : 1], kj[KM == kVar ? KPT : 1];
     const uint64_t kvo0 = KM == kVar ? gld(ks.off0) : 0;
     // bytes of the batch's key data from ks.data: a key may be over-read up to its 16-byte
     // multiple (murmur_seeds_ua) when that stays inside them
@@ -328,12 +279,9 @@ __global__ void __launch_bounds__(kPartThreads) k_part(KeySet ks, uint64_t n, in
                 kw[u] = ld_stream_nt<kNtKeys>(reinterpret_cast<const uint32_t*>(ks.data) + i * 4);
             }
         } else if constexpr (KM == kVar) {
-            // with a length ranking (k_len_rank) thread slot r hashes the sub-chunk's key of rank r
 #pragma unroll
             for (int u = 0; u < KPT; ++u) {
-                const uint64_t slot = min(s0 + u * nt + tid, n - 1);
-                kpj[u] = ks.perm ? uint32_t(gld(ks.perm + slot)) : uint32_t(slot - s0);
-                const uint64_t i = min(s0 + kpj[u], n - 1);
+                const uint64_t i = min(s0 + u * nt + tid, n - 1);
                 koa[u] = gld(ks.offsets + i);
                 kob[u] = gld(ks.offsets + i + 1);
             }
@@ -348,7 +296,6 @@ __global__ void __launch_bounds__(kPartThreads) k_part(KeySet ks, uint64_t n, in
         const uint64_t s1 = min(k1, s0 + pg.kps);
 #pragma unroll
         for (int u = 0; u < KPT; ++u) {
-            if constexpr (KM == kVar) kj[u] = kpj[u];
             const uint64_t i = s0 + u * nt + tid;
             auto emit = [&](int s, uint32_t h) {
                 const uint32_t p = tile_pos(h, tm);
@@ -369,7 +316,7 @@ __global__ void __launch_bounds__(kPartThreads) k_part(KeySet ks, uint64_t n, in
                         murmur_seeds_seg<KMAX>(ks.data + a, len, k, emit);
                 }
                 else
-                    hash_key<KMAX, KM>(ks, KM == kVar ? s0 + kpj[u] : i, k, emit);
+                    hash_key<KMAX, KM>(ks, i, k, emit);
             }
         }
     };
@@ -454,16 +401,14 @@ __global__ void __launch_bounds__(kPartThreads) k_part(KeySet ks, uint64_t n, in
         }
 #pragma unroll
         for (int u = 0; u < KPT; ++u) {
-            const uint32_t slot_key = u * nt + tid;  // the thread slot (liveness)
-            uint32_t key_of = slot_key;               // the key's own index in the sub-chunk
-            if constexpr (KM == kVar) key_of = kj[u];
+            const uint32_t slot_key = u * nt + tid;
             if (uint32_t(u) < kpt && s0 + slot_key < s1) {
 #pragma unroll
                 for (int s = 0; s < KMAX; ++s) {
                     if (s < k) {
                         const uint32_t p = pos[u * KMAX + s];
                         const uint32_t slot = HOIST ? rk[u * KMAX + s] : lbase[p >> tm.tb] + rk[u * KMAX + s];
-                        stage[slot] = PROBE ? (((gkey0 + key_of) << kSlotShift) | (p & lmask)) : p;
+                        stage[slot] = PROBE ? (((gkey0 + slot_key) << kSlotShift) | (p & lmask)) : p;
                         if constexpr (PROBE) bkt[slot] = uint16_t(p >> tm.tb);
                     }
                 }
