@@ -145,49 +145,6 @@ __device__ __forceinline__ void murmur_seeds_seg(const uint8_t* p, uint32_t len,
         if (s < k) emit(s, fmix32(h[s] ^ len));
 }
 
-// murmur_seeds_seg for a key whose bytes may be over-read: [p, p + 16 * ceil(len / 16)) must be
-// readable (the caller checks it against the end of the batch's key bytes).  gfx950 runs in the
-// unaligned access mode, so 16-byte loads at the key's own byte address return its words in
-// order (tools/microbench/unaligned_loads.hip: every byte offset 0..15 exact): no aligned chunk
-// window, no barrel shift, no alignbyte per block; the tail's dword is one unaligned load.
-template <int KMAX, class Emit>
-__device__ __forceinline__ void murmur_seeds_ua(const uint8_t* p, uint32_t len, int k, Emit&& emit, int sbase = 0) {
-    uint32_t h[KMAX];
-#pragma unroll
-    for (int s = 0; s < KMAX; ++s) h[s] = uint32_t(sbase + s);
-    const uint32_t nb = len >> 2, t = len & 3;
-    const uint32_t nch = (len + 15) >> 4;
-    const uint32_t tail = t ? (gld(reinterpret_cast<const uint32_t*>(p + 4 * nb)) & ((1u << (8 * t)) - 1u)) : 0u;
-    for (uint32_t seg = 0; seg * 16 < nb; ++seg) {
-        uint32_t W[16];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            const uint4 v = gld(reinterpret_cast<const uint4*>(p + 16 * min(4 * seg + c, nch - 1)));
-            W[4 * c] = v.x;
-            W[4 * c + 1] = v.y;
-            W[4 * c + 2] = v.z;
-            W[4 * c + 3] = v.w;
-        }
-        const uint32_t nbs = min(nb - 16 * seg, 16u);
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            if (uint32_t(j) < nbs) {
-                const uint32_t km = mix_block(W[j]);
-#pragma unroll
-                for (int s = 0; s < KMAX; ++s) h[s] = round_h(h[s], km);
-            }
-        }
-    }
-    if (t) {
-        const uint32_t km = mix_block(tail);
-#pragma unroll
-        for (int s = 0; s < KMAX; ++s) h[s] ^= km;
-    }
-#pragma unroll
-    for (int s = 0; s < KMAX; ++s)
-        if (s < k) emit(s, fmix32(h[s] ^ len));
-}
-
 // Fixed 16-byte keys from one 16-byte load (the C2/C4/C5 key shape).
 // The first round, rotl(seed ^ m0, 13), is rotl(m0, 13) ^ rotl(seed, 13): the key's part is
 // rotated once for all seeds, the seed's part is uniform (scalar) — one vector op per seed saved.

@@ -120,6 +120,10 @@ size_t stage_bytes() {
 // capped pipelines at 2^30 positions: C4's 125M-key filters (1.25G positions) ran as 107M + 18M
 // keys, and the second pipeline's tile pass streamed the whole 225 MB bitmap again for 18M keys.
 constexpr uint64_t kMaxPositions = (uint64_t(1) << 32) - (uint64_t(1) << 26);
+// Probes keep 2^30 per pipeline: C3's 200M keys in ONE pipeline (G = 512, a 390K-key gather key
+// bitmap per workgroup) measured 14.8 vs 12.9 ms for two of 100M (profiles/r04/s4): the gather's
+// LDS then admits half the workgroups per CU.
+constexpr uint64_t kMaxProbePositions = uint64_t(1) << 30;
 
 // Words loaded in the direct probe's first stage (k_probe): 2 measured best of 1/2/6
 // (profiles/r02/s1, the direct probe is the small-batch path).
@@ -992,7 +996,7 @@ uint64_t tiled_probe_batch(pbf_filter_t* f, int km, uint32_t nf, uint64_t total)
         return pl.lds_gather <= 156 * 1024 && pl.pg.cap <= 65535 &&
                uint64_t(pl.pg.G) * f->tm.nbuckets * (pl.pg.cap / 32) < (uint64_t(1) << 32);
     };
-    const uint64_t top = std::max<uint64_t>(64, (kMaxPositions / k) & ~uint64_t(63));
+    const uint64_t top = std::max<uint64_t>(64, (kMaxProbePositions / k) & ~uint64_t(63));
     uint64_t n = top;
     while (n > 64 * 1024 && !fits(n)) n = std::max<uint64_t>(64 * 1024, (n / 2) & ~uint64_t(63));
     if (n < top && n >= 64 * 1024) {

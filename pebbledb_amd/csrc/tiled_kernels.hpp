@@ -268,9 +268,6 @@ __global__ void __launch_bounds__(kPartThreads) k_part(KeySet ks, uint64_t n, in
     uint4 kw[KM == kFixed16 ? KPT : 1];
     uint64_t koa[KM == kVar ? KPT : 1], kob[KM == kVar ? KPT : 1];
     const uint64_t kvo0 = KM == kVar ? gld(ks.off0) : 0;
-    // bytes of the batch's key data from ks.data: a key may be over-read up to its 16-byte
-    // multiple (murmur_seeds_ua) when that stays inside them
-    const uint64_t kvend = KM == kVar && n ? gld(ks.offsets + n) - kvo0 : 0;
     auto load_keys = [&](uint64_t s0) {
         if constexpr (KM == kFixed16) {
 #pragma unroll
@@ -305,16 +302,8 @@ __global__ void __launch_bounds__(kPartThreads) k_part(KeySet ks, uint64_t n, in
             if (uint32_t(u) < kpt && i < s1) {
                 if constexpr (KM == kFixed16)
                     murmur_seeds16<KMAX>(kw[u], k, emit);
-                else if constexpr (KM == kVar && KMAX > 0) {
-                    const uint64_t a = koa[u] - kvo0;
-                    const uint32_t len = uint32_t(kob[u] - koa[u]);
-#ifndef PBF_AB_ALIGNED_HASH  // (A/B only, round 4: the aligned-chunk hash for every key)
-                    if (a + ((uint64_t(len) + 15) & ~uint64_t(15)) <= kvend)
-                        murmur_seeds_ua<KMAX>(ks.data + a, len, k, emit);
-                    else
-#endif
-                        murmur_seeds_seg<KMAX>(ks.data + a, len, k, emit);
-                }
+                else if constexpr (KM == kVar && KMAX > 0)
+                    murmur_seeds_seg<KMAX>(ks.data + (koa[u] - kvo0), uint32_t(kob[u] - koa[u]), k, emit);
                 else
                     hash_key<KMAX, KM>(ks, i, k, emit);
             }

@@ -65,6 +65,7 @@ for step in "$@"; do
     pmcall) run pmcall 2400 tools/pmc_passes.sh gpurun_out/pmcall ;;
     pmc_c3) run pmc_c3 2400 tools/pmc_passes.sh gpurun_out/pmc_c3 --config c3 ;;
     pmc_c4) run pmc_c4 2400 tools/pmc_passes.sh gpurun_out/pmc_c4 --config c4 ;;
+    pmc_c4s) PBF_STREAMS=1 run pmc_c4s 2400 tools/pmc_passes.sh gpurun_out/pmc_c4s --config c4 ;;
     bench_c1) run bench_c1 300 python bench.py --config c1 --steps 50 --warmup 5 ;;
     bench_c3) run bench_c3 600 python bench.py --config c3 --steps 5 --warmup 2 ;;
     bench_c4) run bench_c4 600 python bench.py --config c4 --steps 3 --warmup 1 ;;
