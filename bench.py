@@ -59,6 +59,8 @@ def parse():
     ap.add_argument("--sync-each-step", action="store_true", help="diagnostic: synchronise after every step")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the bounded CPU sample")
     ap.add_argument("--no-host-c5", action="store_true", help="c5: skip the host-resident (pinned H2D) leg")
+    ap.add_argument("--no-compare", action="store_true",
+                    help="c5: skip the per-filter comparison leg (PMC passes of the fused probe alone)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher / rendezvous check only (gloo, no GPU work, no measurement)")
     return ap.parse_args()
@@ -554,7 +556,7 @@ def sets_main(args, rank, world, local, torch, dist, np):
             if world == 1 and not args.no_cpu_baseline:
                 out["cpu_baseline"] = c5_cpu_baseline(args, filters, mine, hms, q, n_f, nb_bytes, k, np)
                 out["check"]["oracle_sample_equal"] = out["cpu_baseline"].pop("oracle_sample_equal")
-        if args.config == "c5":
+        if args.config == "c5" and not args.no_compare:
             # the same work as independent single-filter probes (no shared partition)
             tq = []
             for _ in range(2):

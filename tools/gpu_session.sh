@@ -61,7 +61,7 @@ for step in "$@"; do
     traffic) traffic c2 --steps 5 --warmup 2 ;;
     traffic_c3) TRAFFIC_ARGS="--probe-scale 2.0" traffic c3 --config c3 --steps 2 --warmup 1 ;;  # two equal 100M-key pipelines per probe pass
     traffic_c4) traffic c4 --config c4 --steps 2 --warmup 1 ;;  # per-filter build pass (bench scales by the rank's filters)
-    traffic_c5) TRAFFIC_ARGS="--probe-scale 3.0" traffic c5 --config c5 --steps 2 --warmup 1 --no-host-c5 ;;  # three equal pipelines
+    traffic_c5) TRAFFIC_ARGS="--probe-scale 3.0" traffic c5 --config c5 --steps 2 --warmup 1 --no-host-c5 --no-compare ;;  # three equal pipelines
     pmcall) run pmcall 2400 tools/pmc_passes.sh gpurun_out/pmcall ;;
     pmc_c3) run pmc_c3 2400 tools/pmc_passes.sh gpurun_out/pmc_c3 --config c3 ;;
     pmc_c4) run pmc_c4 2400 tools/pmc_passes.sh gpurun_out/pmc_c4 --config c4 ;;
@@ -108,7 +108,8 @@ for step in "$@"; do
              traffic c2 --steps 5 --warmup 2 ;;
     final_b) TRAFFIC_ARGS="--probe-scale 2.0" traffic c3 --config c3 --steps 2 --warmup 1
              traffic c4 --config c4 --steps 2 --warmup 1
-             TRAFFIC_ARGS="--probe-scale 3.0" traffic c5 --config c5 --steps 2 --warmup 1 --no-host-c5 ;;
+             TRAFFIC_ARGS="--probe-scale 3.0" traffic c5 --config c5 --steps 2 --warmup 1 --no-host-c5 --no-compare ;;
+    traffic_c5b) TRAFFIC_ARGS="--probe-scale 3.0" traffic c5 --config c5 --steps 2 --warmup 1 --no-host-c5 --no-compare ;;
     final_c) run bench_c1 300 python bench.py --config c1 --steps 50 --warmup 5
              PBF_SHARED_READERS=0 run bench_c1_excl 300 python bench.py --config c1 --steps 50 --warmup 5
              run bench_c3 600 python bench.py --config c3 --steps 5 --warmup 2
