@@ -59,6 +59,7 @@ extern "C" {
 #define PBF_DETAIL_SORT 2    /* tiled: counting-sort partition (k_part) */
 #define PBF_DETAIL_ONE_KEY 4 /* pbf_may_contain's one-key launch */
 #define PBF_DETAIL_SET 8     /* multi-filter direct probe (k_probe_set: each key hashed once for the set) */
+#define PBF_DETAIL_PACKED 16 /* tiled build: region entries packed three positions per 8 bytes */
 
 typedef struct pbf_filter pbf_filter_t;
 
@@ -195,7 +196,7 @@ int pbf_last_build_mode(pbf_filter_t* f);
 int pbf_set_probe_mode(pbf_filter_t* f, int mode);
 int pbf_last_probe_mode(pbf_filter_t* f);
 uint32_t pbf_last_probe_detail(pbf_filter_t* f);
-/* How the last tiled build ran: PBF_DETAIL_RING or _SORT | (keys per sub-chunk / 256) << 12. */
+/* How the last tiled build ran: PBF_DETAIL_RING or _SORT [| _PACKED] | (keys per sub-chunk / 256) << 12. */
 uint32_t pbf_last_build_detail(pbf_filter_t* f);
 
 /* Release the device's pooled working memory (waits for its last users); the next call

@@ -19,7 +19,7 @@ PBF_ERR_HIP = -2
 PBF_ERR_ZERO_SIZE = -3
 PBF_BUILD_AUTO, PBF_BUILD_ATOMIC, PBF_BUILD_TILED = 0, 1, 2
 PBF_PROBE_AUTO, PBF_PROBE_DIRECT, PBF_PROBE_TILED = 0, 1, 2
-PBF_DETAIL_RING, PBF_DETAIL_SORT, PBF_DETAIL_ONE_KEY, PBF_DETAIL_SET = 1, 2, 4, 8
+PBF_DETAIL_RING, PBF_DETAIL_SORT, PBF_DETAIL_ONE_KEY, PBF_DETAIL_SET, PBF_DETAIL_PACKED = 1, 2, 4, 8, 16
 
 _u8p = ctypes.c_void_p
 _vp = ctypes.c_void_p

@@ -590,6 +590,7 @@ int run_atomic(pbf_filter_t* f, const Batch& b) {
 // Geometry of the partition pass for a batch of n keys (see tiled_kernels.hpp).
 struct PartPlan {
     PartGeom pg;
+    bool pk3;           // counting-sort build with packed entries (k_part / k_tile_build PK3)
     size_t lds_part;
     size_t lds_gather;  // probes: per gather workgroup
     uint32_t gsplit;    // probes: gather splits over tile ranges (grid G x gsplit)
@@ -685,6 +686,15 @@ int part_kmax(uint32_t k, int km) {
     return kmax_for(k);
 }
 
+// Packed build entries (PBF_PK3=0 disables them, for A/B measurements).
+bool pk3_enabled() {
+    static const bool v = [] {
+        const char* e = std::getenv("PBF_PK3");
+        return !(e && e[0] == '0');
+    }();
+    return v;
+}
+
 PartPlan plan_partition(uint32_t B, uint32_t k, int km, uint64_t n, bool probe, double share, uint32_t nf) {
     PartPlan pl{};
     const size_t per_entry = probe ? 6 : 4;  // stage u32 (+ u16 tile id for probes)
@@ -696,6 +706,11 @@ PartPlan plan_partition(uint32_t B, uint32_t k, int km, uint64_t n, bool probe, 
     if (probe) kpt = kpt >= 4 ? 4 : (kpt >= 2 ? 2 : 1);
     const uint64_t kps = kpt * kPartThreads;
     pl.lds_part = fixed + size_t(kps) * k * per_entry;
+    // packed build entries (tiled_kernels.hpp PK3) for the exact-k kernels when the padded stage
+    // (<= 2 pad slots per tile) fits the CU's LDS at the same sub-chunk size
+    const size_t pk3_lds = pl.lds_part + 8 * std::min<size_t>(B, size_t(kps) * k);
+    pl.pk3 = !probe && pk3_enabled() && km != kFixedN && (k == 6 || k == 8 || k == 10) && pk3_lds <= 160 * 1024;
+    if (pl.pk3) pl.lds_part = pk3_lds;
     const uint64_t G0 = std::min<uint64_t>(part_max_groups(probe), std::max<uint64_t>(1, (n + kps - 1) / kps));
     uint64_t kpw = (n + G0 - 1) / G0;
     kpw = ((kpw + kps - 1) / kps) * kps;
@@ -709,6 +724,11 @@ PartPlan plan_partition(uint32_t B, uint32_t k, int km, uint64_t n, bool probe, 
     // (k_part addresses an entry by a 24-bit multiply-add within its workgroup's regions)
     pl.pg.cap = uint32_t(std::min<uint64_t>(((cap + 31) / 32) * 32, ((uint64_t(1) << 32) - 1) / std::max<uint32_t>(B, 1) & ~uint64_t(31)));
     pl.pg.cap = std::min<uint32_t>(pl.pg.cap, (1u << 24) - 32);
+    if (pl.pk3) {
+        // + the pads (<= 2 per sub-chunk), in whole 32-word units of 3 entries
+        const uint64_t c3 = uint64_t(pl.pg.cap) + 2 * pl.pg.nsub;
+        pl.pg.cap = uint32_t(std::min<uint64_t>(((c3 + 95) / 96) * 96, ((1u << 24) - 96) / 96 * 96));
+    }
     set_gather(pl, B, pl.pg.nq + 1, nf);
     return pl;
 }
@@ -770,14 +790,14 @@ void with_ring_kernel(uint32_t k, bool pow2, L&& launch) {
 // The counting-sort partition kernel for (k, key layout): exact-k variants for the k the
 // configurations use (6: C2/C5 shapes, 8: C3, 10: the fp = 0.001 product sizing of C4 / SSTables).
 template <int KX, int KMD, bool PROBE, class L>
-void with_part_kernel(uint32_t k, L&& launch) {
+void with_part_kernel(uint32_t k, L&& launch, bool pk3 = false) {
     if constexpr (KMD != kFixedN) {
         if constexpr (KX == 8) {
-            if (k == 6) return launch(k_part<6, KMD, PROBE, true>);
-            if (k == 8) return launch(k_part<8, KMD, PROBE, true>);
+            if (k == 6) return pk3 && !PROBE ? launch(k_part<6, KMD, PROBE, true, true>) : launch(k_part<6, KMD, PROBE, true>);
+            if (k == 8) return pk3 && !PROBE ? launch(k_part<8, KMD, PROBE, true, true>) : launch(k_part<8, KMD, PROBE, true>);
         }
         if constexpr (KX == 16) {
-            if (k == 10) return launch(k_part<10, KMD, PROBE, true>);
+            if (k == 10) return pk3 && !PROBE ? launch(k_part<10, KMD, PROBE, true, true>) : launch(k_part<10, KMD, PROBE, true>);
         }
     }
     launch(k_part<KX, KMD, PROBE>);
@@ -824,17 +844,23 @@ int run_tiled(pbf_filter_t* f, const Batch& b) {
                     if (err == hipSuccess)
                         kern<<<pg.G, kPartThreads, pl.lds_part, s>>>(pks, b.n, int(k), tm, pg, regions, fill, nullptr,
                                                              ovf, ovf_count, ProbeSet{}, nullptr);
-                });
+                }, pl.pk3);
             }
         }
     });
     HIP_TRY(err);
     LAUNCHED(f, pg.ring ? "k_part_ring<build>" : "k_part<build>");
     const size_t lds_tile = ((size_t(1) << tm.tb) / 32 + pg.G) * 4;
-    HIP_TRY(allow_lds(k_tile_build, lds_tile));
-    k_tile_build<<<B, 1024, lds_tile, s>>>(tm, pg, regions, fill, f->bitmap, f->pristine ? 1 : 0);
+    if (pl.pk3) {
+        HIP_TRY(allow_lds(k_tile_build<true>, lds_tile));
+        k_tile_build<true><<<B, 1024, lds_tile, s>>>(tm, pg, regions, fill, f->bitmap, f->pristine ? 1 : 0);
+    } else {
+        HIP_TRY(allow_lds(k_tile_build<false>, lds_tile));
+        k_tile_build<false><<<B, 1024, lds_tile, s>>>(tm, pg, regions, fill, f->bitmap, f->pristine ? 1 : 0);
+    }
     LAUNCHED(f, "k_tile_build");
-    f->last_build_detail = (pg.ring ? PBF_DETAIL_RING : PBF_DETAIL_SORT) | ((pg.kps / 256) << 12);
+    f->last_build_detail = (pg.ring ? PBF_DETAIL_RING : PBF_DETAIL_SORT) | (pl.pk3 ? PBF_DETAIL_PACKED : 0u) |
+                           ((pg.kps / 256) << 12);
     k_ovf_build<<<256, 256, 0, s>>>(tm, ovf, ovf_count, f->bitmap, ovf_next);
     LAUNCHED(f, "k_ovf_build");
     f->pristine = false;

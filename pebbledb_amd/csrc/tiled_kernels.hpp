@@ -217,8 +217,17 @@ __host__ __device__ constexpr int part_kpt(int kmax, int km, bool probe) {
     return kmax <= 4 ? 4 : (kmax <= 8 ? 2 : 1);
 }
 
+// Packed build entries (PK3): a region holds 8-byte words of three 21-bit positions in the tile
+// (bits 0-20, 21-41, 42-62), so the partition writes and the tile build reads 8 B per 3 positions
+// instead of 12.  Each tile's run of a sub-chunk is padded to a multiple of 3 in the stage: the
+// scan writes a pad value of another tile ((b ^ 1) << tb) into the 0-2 slots past the run, and
+// the write-out replaces a pad by the word's first position (setting a bit twice is harmless).
+// Region cursors and capacities stay in entries (multiples of 3); fill counts are in words.
+constexpr uint32_t kPk3Bits = 21;
+__device__ __forceinline__ uint32_t div3(uint32_t x) { return __umulhi(x, 0xAAAAAAABu) >> 1; }
+
 // EXACT: k == KMAX at compile time (no per-seed branches; the seeds' LDS atomics issue together).
-template <int KMAX, int KM, bool PROBE, bool EXACT = false>
+template <int KMAX, int KM, bool PROBE, bool EXACT = false, bool PK3 = false>
 __global__ void __launch_bounds__(kPartThreads) k_part(KeySet ks, uint64_t n, int k, TileMap tm, PartGeom pg,
                                                        uint32_t* __restrict__ regions, uint32_t* __restrict__ fill,
                                                        uint16_t* __restrict__ pref, uint32_t* __restrict__ ovf,
@@ -314,16 +323,19 @@ __global__ void __launch_bounds__(kPartThreads) k_part(KeySet ks, uint64_t n, in
     // + its count - lbase[b]); a previous sub-chunk that closed a 4096-key group leaves the
     // routed count cb[b] + lbase_prev[b + 1] in pref.  A thread scans <= 4 tiles (B <= 4096).
     // Ends synced.
+    auto padded = [](uint32_t c) { return PK3 ? c + (3u - c % 3u) % 3u : c; };
     auto scan_advance = [&](bool group_end, uint32_t q) {
         const uint32_t per = (B + nt - 1) / nt;
         const uint32_t lo = min(B, tid * per), hi = min(B, lo + per);
-        uint32_t sum = 0, prevn[4];
+        uint32_t sum = 0, prevn[4], cn[4];
 #pragma unroll
         for (int x = 0; x < 4; ++x) {
             const uint32_t b = lo + x;
             prevn[x] = 0;
+            cn[x] = 0;
             if (b < hi) {
-                sum += cnt[b];
+                cn[x] = cnt[b];
+                sum += padded(cn[x]);
                 prevn[x] = lbase[b + 1];
             }
         }
@@ -356,7 +368,13 @@ __global__ void __launch_bounds__(kPartThreads) k_part(KeySet ks, uint64_t n, in
                 if (PROBE && group_end) pref[(uint64_t(g) * nqs + q) * B + b] = uint16_t(min(c, pg.cap));
                 cb[b] = c - run;
                 lbase[b] = run;
-                run += cnt[b];
+                if constexpr (PK3) {
+                    const uint32_t pc = padded(cn[x]);
+                    for (uint32_t y = cn[x]; y < pc; ++y) stage[run + y] = (b ^ 1u) << tm.tb;
+                    run += pc;
+                } else {
+                    run += cn[x];
+                }
             }
         }
         if (tid == nt - 1) lbase[B] = run;
@@ -420,6 +438,47 @@ __global__ void __launch_bounds__(kPartThreads) k_part(KeySet ks, uint64_t n, in
         // (four per batch when the next sub-chunk's KPT x KMAX positions and ranks already hold
         // 60 registers: C4's k = 10 build, which spills at eight)
         constexpr int UW = KPT * KMAX >= 30 ? 4 : 8;
+        if constexpr (PK3) {
+            // one 8-byte word (three stage entries of one tile) per thread and batch slot
+            uint64_t* const rgn64 = reinterpret_cast<uint64_t*>(regions) + uint64_t(g) * B * (pg.cap / 3);
+            const uint32_t capw = pg.cap / 3, totw = tot / 3;
+            for (uint32_t w0 = tid; w0 < totw; w0 += nt * UW) {
+                uint32_t v0[UW], v1[UW], v2[UW], b[UW], r[UW];
+#pragma unroll
+                for (int u = 0; u < UW; ++u) {
+                    const uint32_t e = 3 * min(w0 + u * nt, totw - 1);
+                    v0[u] = stage[e];
+                    v1[u] = stage[e + 1];
+                    v2[u] = stage[e + 2];
+                    b[u] = v0[u] >> tm.tb;
+                }
+#pragma unroll
+                for (int u = 0; u < UW; ++u) r[u] = cb[b[u]] + 3 * (w0 + u * nt);
+                uint32_t over = 0;
+#pragma unroll
+                for (int u = 0; u < UW; ++u) {
+                    const bool live = w0 + u * nt < totw;
+                    const uint32_t a = v0[u] & lmask;
+                    const uint32_t c1 = (v1[u] >> tm.tb) == b[u] ? (v1[u] & lmask) : a;
+                    const uint32_t c2 = (v2[u] >> tm.tb) == b[u] ? (v2[u] & lmask) : a;
+                    const uint64_t word = uint64_t(a) | (uint64_t(c1) << kPk3Bits) | (uint64_t(c2) << (2 * kPk3Bits));
+                    if (live && r[u] < pg.cap) rgn64[__umul24(b[u], capw) + div3(r[u])] = word;
+                    over |= uint32_t(live && r[u] >= pg.cap) << u;
+                }
+                if (over) {  // region overflow: heavy key duplication only
+#pragma unroll
+                    for (int u = 0; u < UW; ++u) {
+                        if ((over >> u) & 1u) {
+                            const uint32_t x = atomicAdd(ovf_count, 3u);
+                            ovf[x] = v0[u];
+                            ovf[x + 1] = (v1[u] >> tm.tb) == b[u] ? v1[u] : v0[u];
+                            ovf[x + 2] = (v2[u] >> tm.tb) == b[u] ? v2[u] : v0[u];
+                        }
+                    }
+                }
+            }
+            continue;
+        }
         for (uint32_t e0 = tid; e0 < tot; e0 += nt * UW) {
             uint32_t v[UW], b[UW], r[UW];
 #pragma unroll
@@ -454,7 +513,7 @@ __global__ void __launch_bounds__(kPartThreads) k_part(KeySet ks, uint64_t n, in
     lds_barrier();
     for (uint32_t b = tid; b < B; b += nt) {
         const uint32_t t = min(cb[b] + lbase[b + 1], pg.cap);
-        fill[uint64_t(b) * pg.G + g] = t;
+        fill[uint64_t(b) * pg.G + g] = PK3 ? t / 3 : t;
         if constexpr (PROBE)  // the open last group and any the workgroup did not reach
             for (uint32_t q = (j + spg - 1) / spg; q <= pg.nq; ++q) pref[(uint64_t(g) * nqs + q) * B + b] = uint16_t(t);
     }
@@ -503,14 +562,39 @@ __device__ __forceinline__ void or_bits4(uint32_t* tile, uint4 v, uint32_t e, ui
     }
 }
 
+// OR the in-fill words of a 16-byte piece of packed (PK3) words into the LDS tile: word e
+// (positions bits 0-20, 21-41, 42-62) and, when e + 1 < f, word e + 1.
+__device__ __forceinline__ void or_bits_pk3(uint32_t* tile, uint4 v, uint32_t e, uint32_t f, uint32_t lmask) {
+    const uint32_t lo[2] = {v.x, v.z}, hi[2] = {v.y, v.w};
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        if (e + q < f) {
+            const uint32_t p0 = lo[q] & lmask;
+            const uint32_t p1 = __builtin_amdgcn_alignbit(hi[q], lo[q], kPk3Bits) & lmask;
+            const uint32_t p2 = (hi[q] >> (2 * kPk3Bits - 32)) & lmask;
+            atomicOr(tile + (p0 >> 5), 1u << (p0 & 31));
+            atomicOr(tile + (p1 >> 5), 1u << (p1 & 31));
+            atomicOr(tile + (p2 >> 5), 1u << (p2 & 31));
+        }
+    }
+}
+
 // ------------------------------------------------------------------ build: tiles
-// One workgroup per tile.  A wave (64 lanes x 16-byte loads = 256 entries) covers one region
-// per step and keeps kTileBuildRegionsInFlight regions of loads in flight.
+// One workgroup per tile.  A wave (64 lanes x 16-byte loads = 256 entries, or 128 packed words)
+// covers one region per step and keeps kTileBuildRegionsInFlight regions of loads in flight.
+// PK3: regions of packed words (k_part's PK3), `fill` in words, region stride cap / 3 words.
+template <bool PK3>
 __global__ void __launch_bounds__(1024) k_tile_build(TileMap tm, PartGeom pg, const uint32_t* __restrict__ regions,
                                                      const uint32_t* __restrict__ fill, uint32_t* __restrict__ bitmap,
                                                      int pristine) {
     extern __shared__ uint32_t smem[];
-    const uint32_t B = tm.nbuckets, G = pg.G, cap = pg.cap;
+    // cap in 4-byte units: entries, or the packed words' dwords
+    const uint32_t B = tm.nbuckets, G = pg.G, cap = PK3 ? 2 * (pg.cap / 3) : pg.cap;
+    constexpr uint32_t PER = PK3 ? 2 : 4;  // fill units (entries / words) per 16-byte load
+    auto or16 = [&](uint32_t* t, uint4 v, uint32_t e, uint32_t f, uint32_t lm) {
+        if constexpr (PK3) or_bits_pk3(t, v, e, f, lm);
+        else or_bits4(t, v, e, f, lm);
+    };
     const uint32_t b = blockIdx.x;
     const uint32_t W = 1u << (tm.tb - 5);
     uint32_t* tile = smem;       // W
@@ -538,12 +622,12 @@ __global__ void __launch_bounds__(1024) k_tile_build(TileMap tm, PartGeom pg, co
                 const uint32_t q = g0 + u * nwaves;
                 f[u] = q < G ? fills[q] : 0u;
                 // unconditional loads, clamped to the filled part (idle lanes re-read its last line)
-                const uint32_t lc = min(lane, (max(f[u], 1u) - 1) >> 2);
+                const uint32_t lc = min(lane, (max(f[u], 1u) - 1) / PER);
                 v[u] = ld_stream_nt<kNtLoad>(regions + region_id(min(q, G - 1), b, G, B) * cap + lc * 4);
             }
 #pragma unroll
             for (int u = 0; u < U; ++u)
-                if (lane * 4 < f[u]) or_bits4(tile, v[u], lane * 4, f[u], lmask);
+                if (lane * PER < f[u]) or16(tile, v[u], lane * PER, f[u], lmask);
         }
     } else {
         // regions of many chunks (C4: ~2,850 entries, C3: ~760): the wave walks the (region,
@@ -556,21 +640,22 @@ __global__ void __launch_bounds__(1024) k_tile_build(TileMap tm, PartGeom pg, co
             uint32_t f[U], e[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                while (q < G && c * 256 >= fills[q]) {
+                while (q < G && c * 64 * PER >= fills[q]) {
                     q += nwaves;
                     c = 0;
                 }
                 const bool live = q < G;
                 f[u] = live ? fills[q] : 0u;
-                e[u] = c * 256 + lane * 4;
+                e[u] = (c * 64 + lane) * PER;
                 const uint32_t qq = live ? q : G - 1, fq = live ? f[u] : 1u;
-                const uint32_t ec = min(e[u], (fq - 1) & ~3u);  // clamped: idle lanes re-read a filled line
+                // clamped: idle lanes re-read a filled line
+                const uint32_t ec = min(e[u] / PER, (fq - 1) / PER) * 4;
                 v[u] = ld_stream_nt<kNtLoad>(regions + region_id(qq, b, G, B) * cap + ec);
                 if (live) ++c;
             }
 #pragma unroll
             for (int u = 0; u < U; ++u)
-                if (e[u] < f[u]) or_bits4(tile, v[u], e[u], f[u], lmask);
+                if (e[u] < f[u]) or16(tile, v[u], e[u], f[u], lmask);
         }
     }
     lds_barrier();

@@ -348,7 +348,7 @@ def test_sstable_section_roundtrip_golden():
 
 
 _PART_CHILD = """
-import numpy as np, sys
+import numpy as np, os, sys
 sys.path.insert(0, '.')
 from pebbledb_amd import BloomFilter, PackedKeys, _native
 from pebbledb_amd.keys import splitmix_hex_keys, varlen_keys
@@ -373,19 +373,21 @@ for nb, pk, q in ((2 ** 27, fx, probes), (3 * 2 ** 25, vr, vr), (2 ** 21, fx, pr
     bf.set_probe_mode(2)
     assert np.array_equal(bf.may_contain_many(q, packed=True), want_hm), nb
     assert bf.last_probe_mode == 2 and bf.last_build_mode == 2
+    if os.environ.get('PBF_PART') == 'sort':  # exact k = 6: packed entries unless disabled
+        assert bool(bf.last_build_detail & _native.PBF_DETAIL_PACKED) == (os.environ.get('PBF_PK3') != '0'), hex(bf.last_build_detail)
 print('ok')
 """
 
 
-@pytest.mark.parametrize("part", ["sort", "ring"])
-def test_tiled_partition_strategies_and_region_overflow(part):
-    """Both partition passes of the tiled build / probe (PBF_PART forces one), with a key
-    repeated enough to overflow its tiles' regions and rings (build overflow list, probe
-    in-place test)."""
+@pytest.mark.parametrize("part,pk3", [("sort", "1"), ("sort", "0"), ("ring", "1")])
+def test_tiled_partition_strategies_and_region_overflow(part, pk3):
+    """Both partition passes of the tiled build / probe (PBF_PART forces one; the counting sort's
+    build with packed and plain region entries, PBF_PK3), with a key repeated enough to overflow
+    its tiles' regions and rings (build overflow list, probe in-place test)."""
     import os
     import subprocess
     import sys
-    env = dict(os.environ, PBF_PART=part)
+    env = dict(os.environ, PBF_PART=part, PBF_PK3=pk3)
     r = subprocess.run([sys.executable, "-c", _PART_CHILD], env=env, capture_output=True, text=True, timeout=600,
                        cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]

@@ -90,6 +90,13 @@ for step in "$@"; do
     abenv) abenv abenv 300 2 --steps 50 --warmup 5 ;;
     abenv_c5) abenv abenvc5 300 1 --config c5 --steps 5 --warmup 2 --no-host-c5 ;;
     abenv_c3) abenv abenvc3 300 2 --config c3 --steps 3 --warmup 1 ;;
+    abenv_c4) abenv abenvc4 400 2 --config c4 --steps 3 --warmup 1 ;;
+    prof_var_c3) for v in build/variants/*.so; do
+                   nm=$(basename $v .so)
+                   PBF_LIB=$PWD/$v prof profv_c3_$nm 300 --config c3 --steps 3 --warmup 1 --no-cpu-baseline --no-host-inclusive
+                 done ;;
+    abenv_c3_1) abenv abenvc3 300 1 --config c3 --steps 3 --warmup 1 ;;
+    abenv_c4_1) abenv abenvc4 400 1 --config c4 --steps 3 --warmup 1 ;;
     bench_c1_excl) PBF_SHARED_READERS=0 run bench_c1_excl 300 python bench.py --config c1 --steps 50 --warmup 5 ;;
     prof_c4_serial) PBF_STREAMS=1 prof prof_c4_serial 600 --config c4 --steps 2 --warmup 1 --no-cpu-baseline ;;
     ab_c3) ab abc3 300 1 --config c3 --steps 3 --warmup 1 ;;
