@@ -699,18 +699,23 @@ PartPlan plan_partition(uint32_t B, uint32_t k, int km, uint64_t n, bool probe, 
     PartPlan pl{};
     const size_t per_entry = probe ? 6 : 4;  // stage u32 (+ u16 tile id for probes)
     const size_t fixed = size_t(3 * B + 1 + 16) * 4;
-    // keys per thread per sub-chunk: as many as the registers (part_kpt) and the LDS allow
+    const uint64_t smax = (156 * 1024 - fixed) / per_entry;  // stage entries the LDS holds
+    // keys per thread per sub-chunk: as many as the registers allow (part_kpt), placed in at most
+    // two windows of the stage
     uint64_t kpt = uint64_t(part_kpt(part_kmax(k, km), km, probe));
-    while (kpt > 1 && fixed + kpt * kPartThreads * k * per_entry > 156 * 1024) --kpt;
+    // (and k_part keeps ranks and slots as 16-bit halves: kps * k + pads < 2^16)
+    while (kpt > 1 && (kpt * kPartThreads * k > 2 * smax || kpt * kPartThreads * k + 2 * std::min<uint64_t>(B, kpt * kPartThreads * k) >= 65536)) --kpt;
     // probe sub-chunks tile the 4096-key groups of the entry format: 1, 2 or 4 keys per thread
     if (probe) kpt = kpt >= 4 ? 4 : (kpt >= 2 ? 2 : 1);
     const uint64_t kps = kpt * kPartThreads;
-    pl.lds_part = fixed + size_t(kps) * k * per_entry;
-    // packed build entries (tiled_kernels.hpp PK3) for the exact-k kernels when the padded stage
-    // (<= 2 pad slots per tile) fits the CU's LDS at the same sub-chunk size
-    const size_t pk3_lds = pl.lds_part + 8 * std::min<size_t>(B, size_t(kps) * k);
-    pl.pk3 = !probe && pk3_enabled() && km != kFixedN && (k == 6 || k == 8 || k == 10) && pk3_lds <= 160 * 1024;
-    if (pl.pk3) pl.lds_part = pk3_lds;
+    // packed build entries (tiled_kernels.hpp PK3) for the exact-k kernels; their runs are padded
+    // (<= 2 pad slots per tile)
+    pl.pk3 = !probe && pk3_enabled() && km != kFixedN && (k == 6 || k == 8 || k == 10);
+    const uint64_t need = kps * k + (pl.pk3 ? 2 * std::min<uint64_t>(B, kps * k) : 0);
+    uint64_t scap = std::min(need, smax);
+    if (pl.pk3) scap -= scap % 3;  // windows hold whole packed words
+    pl.pg.scap = uint32_t(scap);
+    pl.lds_part = fixed + size_t(scap) * per_entry;
     const uint64_t G0 = std::min<uint64_t>(part_max_groups(probe), std::max<uint64_t>(1, (n + kps - 1) / kps));
     uint64_t kpw = (n + G0 - 1) / G0;
     kpw = ((kpw + kps - 1) / kps) * kps;
@@ -793,11 +798,18 @@ template <int KX, int KMD, bool PROBE, class L>
 void with_part_kernel(uint32_t k, L&& launch, bool pk3 = false) {
     if constexpr (KMD != kFixedN) {
         if constexpr (KX == 8) {
-            if (k == 6) return pk3 && !PROBE ? launch(k_part<6, KMD, PROBE, true, true>) : launch(k_part<6, KMD, PROBE, true>);
-            if (k == 8) return pk3 && !PROBE ? launch(k_part<8, KMD, PROBE, true, true>) : launch(k_part<8, KMD, PROBE, true>);
+            if constexpr (!PROBE) {
+                if (pk3 && k == 6) return launch(k_part<6, KMD, PROBE, true, true>);
+                if (pk3 && k == 8) return launch(k_part<8, KMD, PROBE, true, true>);
+            }
+            if (k == 6) return launch(k_part<6, KMD, PROBE, true>);
+            if (k == 8) return launch(k_part<8, KMD, PROBE, true>);
         }
         if constexpr (KX == 16) {
-            if (k == 10) return pk3 && !PROBE ? launch(k_part<10, KMD, PROBE, true, true>) : launch(k_part<10, KMD, PROBE, true>);
+            if constexpr (!PROBE) {
+                if (pk3 && k == 10) return launch(k_part<10, KMD, PROBE, true, true>);
+            }
+            if (k == 10) return launch(k_part<10, KMD, PROBE, true>);
         }
     }
     launch(k_part<KX, KMD, PROBE>);

@@ -122,7 +122,7 @@ struct PartGeom {
     uint32_t nq;       // pref groups (4096 keys each) per workgroup
     uint32_t ring;     // ring partition: LDS ring entries per tile (0 = counting-sort partition)
     uint32_t spill_cap;  // ring partition: entries of the LDS spill buffer
-    uint32_t pad;
+    uint32_t scap;       // counting-sort partition: stage entries (a sub-chunk is placed in windows of scap)
 };
 
 constexpr uint32_t kSlotShift = 20;   // probe entry = key-in-group << 20 | position in tile
@@ -213,8 +213,9 @@ __host__ __device__ constexpr int part_kpt(int kmax, int km, bool probe) {
         if (kmax <= 10 && !probe) return 3;  // the exact k = 10 build (C4's product sizing)
         return kmax <= 16 ? 2 : 1;
     }
-    if (kmax > 4 && kmax <= 8 && !probe) return 3;  // variable-length builds (C3): 3 keys per thread at k = 8
-    return kmax <= 4 ? 4 : (kmax <= 8 ? 2 : 1);
+    // variable-length keys (C3): 4 per thread at k = 8 — 4096-key sub-chunks, placed in windows of
+    // the stage (longer per-tile runs per write-out than the 2048 / 3072 keys a stage holds)
+    return kmax <= 8 ? 4 : 1;
 }
 
 // Packed build entries (PK3): a region holds 8-byte words of three 21-bit positions in the tile
@@ -246,8 +247,8 @@ __global__ void __launch_bounds__(kPartThreads) k_part(KeySet ks, uint64_t n, in
     uint32_t* cnt = cb + B;            // B: the next sub-chunk's per-tile count
     uint32_t* lbase = cnt + B;         // B+1: the current sub-chunk's exclusive scan of its counts
     uint32_t* ws = lbase + B + 1;      // 16
-    uint32_t* stage = ws + 16;         // kps * k
-    uint16_t* bkt = reinterpret_cast<uint16_t*>(stage + pg.kps * uint32_t(k));  // kps * k (probes)
+    uint32_t* stage = ws + 16;         // scap
+    uint16_t* bkt = reinterpret_cast<uint16_t*>(stage + pg.scap);  // scap (probes)
     const uint32_t lmask = (1u << tm.tb) - 1u;
     uint32_t* const rgn = regions + uint64_t(g) * B * pg.cap;  // this workgroup's regions
     // probes: sub-chunks per 4096-key group (kps is 1024, 2048 or 4096 for probes) and the
@@ -295,9 +296,14 @@ __global__ void __launch_bounds__(kPartThreads) k_part(KeySet ks, uint64_t n, in
     };
     // a sub-chunk's positions and their ranks in their tiles (counted into cnt), kept in
     // registers until the sub-chunk is placed
-    uint32_t pos[KPT * KMAX], rk[KPT * KMAX];
+    // (ranks, then global slots, are < 2^16 — kps * k + pads, checked by the host — and kept as
+    // 16-bit halves: entry e in rk2[e / 2] bits 16 * (e % 2))
+    uint32_t pos[KPT * KMAX], rk2[(KPT * KMAX + 1) / 2];
 #pragma unroll
-    for (int e = 0; e < KPT * KMAX; ++e) pos[e] = rk[e] = 0;
+    for (int e = 0; e < KPT * KMAX; ++e) pos[e] = 0;
+#pragma unroll
+    for (int e = 0; e < (KPT * KMAX + 1) / 2; ++e) rk2[e] = 0;
+    auto rank_of = [&](int e) { return (rk2[e >> 1] >> (16 * (e & 1))) & 0xFFFFu; };
     auto hash_count = [&](uint64_t s0) {
         const uint64_t s1 = min(k1, s0 + pg.kps);
 #pragma unroll
@@ -306,7 +312,9 @@ __global__ void __launch_bounds__(kPartThreads) k_part(KeySet ks, uint64_t n, in
             auto emit = [&](int s, uint32_t h) {
                 const uint32_t p = tile_pos(h, tm);
                 pos[u * KMAX + s] = p;
-                rk[u * KMAX + s] = atomicAdd(cnt + (p >> tm.tb), 1u);
+                const uint32_t r = atomicAdd(cnt + (p >> tm.tb), 1u);
+                const int e = u * KMAX + s;
+                rk2[e >> 1] = (e & 1) ? (rk2[e >> 1] & 0xFFFFu) | (r << 16) : r;
             };
             if (uint32_t(u) < kpt && i < s1) {
                 if constexpr (KM == kFixed16)
@@ -368,13 +376,7 @@ __global__ void __launch_bounds__(kPartThreads) k_part(KeySet ks, uint64_t n, in
                 if (PROBE && group_end) pref[(uint64_t(g) * nqs + q) * B + b] = uint16_t(min(c, pg.cap));
                 cb[b] = c - run;
                 lbase[b] = run;
-                if constexpr (PK3) {
-                    const uint32_t pc = padded(cn[x]);
-                    for (uint32_t y = cn[x]; y < pc; ++y) stage[run + y] = (b ^ 1u) << tm.tb;
-                    run += pc;
-                } else {
-                    run += cn[x];
-                }
+                run += padded(cn[x]);
             }
         }
         if (tid == nt - 1) lbase[B] = run;
@@ -391,123 +393,141 @@ __global__ void __launch_bounds__(kPartThreads) k_part(KeySet ks, uint64_t n, in
         const uint64_t s1 = min(k1, s0 + pg.kps);
         lds_barrier();  // this sub-chunk's counts are complete, the previous write-out is done
         scan_advance(PROBE && j > 0 && (j & (spg - 1)) == 0, j / spg);
-        // place the sub-chunk's entries, sorted by tile, into the stage (the key's place in its
-        // 4096-key group goes into a probe entry); cnt is free again
-        // Every tile base is read before the first stage write: interleaved, each write's
-        // address waited on its own LDS read (the compiler cannot tell stage from lbase).  (Not
-        // for the k > 16 register buckets, which would spill.)
-        constexpr bool HOIST = KPT * KMAX < 32;
+        // Place the sub-chunk's entries, sorted by tile, and write them out, in windows of the
+        // stage: entry (tile b, rank r) has the global slot gs = lbase[b] + r of the sub-chunk's
+        // sorted order; window [e_lo, e_lo + scap) is placed into stage[gs - e_lo], then written
+        // out.  A sub-chunk's entries (4096 variable-length keys x 8) may thus exceed the stage:
+        // its per-tile runs, and so the region writes, are as long as the sub-chunk's.  Usually
+        // one or two windows.  (The key's place in its 4096-key group goes into a probe entry.)
         const uint32_t gkey0 = (j & (spg - 1)) * pg.kps;
-        if constexpr (HOIST) {
-#pragma unroll
-            for (int u = 0; u < KPT; ++u) {
-#pragma unroll
-                for (int s = 0; s < KMAX; ++s)
-                    if (s < k) rk[u * KMAX + s] += lbase[pos[u * KMAX + s] >> tm.tb];  // the entry's slot
-            }
-        }
+        const uint32_t tot = lbase[B];
+        const uint32_t S = pg.scap;  // (PK3: a multiple of 3)
 #pragma unroll
         for (int u = 0; u < KPT; ++u) {
-            const uint32_t slot_key = u * nt + tid;
-            if (uint32_t(u) < kpt && s0 + slot_key < s1) {
 #pragma unroll
-                for (int s = 0; s < KMAX; ++s) {
-                    if (s < k) {
-                        const uint32_t p = pos[u * KMAX + s];
-                        const uint32_t slot = HOIST ? rk[u * KMAX + s] : lbase[p >> tm.tb] + rk[u * KMAX + s];
-                        stage[slot] = PROBE ? (((gkey0 + slot_key) << kSlotShift) | (p & lmask)) : p;
-                        if constexpr (PROBE) bkt[slot] = uint16_t(p >> tm.tb);
-                    }
-                }
-            }
+            for (int s = 0; s < KMAX; ++s)
+                if (s < k) rk2[(u * KMAX + s) >> 1] += lbase[pos[u * KMAX + s] >> tm.tb] << (16 * ((u * KMAX + s) & 1));  // the global slot
         }
-        for (uint32_t b = tid; b < B; b += nt) cnt[b] = 0;
-        lds_barrier();
-        // The next sub-chunk is hashed and counted while this one is written out: the hash's
-        // VALU work overlaps the write-out's LDS reads and stores (other waves, same phase).
-        if (s1 < k1) {
-            hash_count(s1);
-            if (s1 + pg.kps < k1) load_keys(s1 + pg.kps);
-        }
-        // Lane-parallel write-out: entry e of the sorted stage goes to position cb[b] + e of
-        // region (g, b).  UW entries per thread per batch: the stage reads, then the cursor
-        // reads, are issued before any is consumed (one LDS wait each), and the
-        // region offsets are 32-bit within the workgroup's regions (B * cap < 2^32; b < 4096,
-        // cap < 2^24: one 24-bit multiply-add).  Positions >= cap overflow (rare).
-        const uint32_t tot = lbase[B];
-        // (four per batch when the next sub-chunk's KPT x KMAX positions and ranks already hold
-        // 60 registers: C4's k = 10 build, which spills at eight)
-        constexpr int UW = KPT * KMAX >= 30 ? 4 : 8;
-        if constexpr (PK3) {
-            // one 8-byte word (three stage entries of one tile) per thread and batch slot
-            uint64_t* const rgn64 = reinterpret_cast<uint64_t*>(regions) + uint64_t(g) * B * (pg.cap / 3);
-            const uint32_t capw = pg.cap / 3, totw = tot / 3;
-            for (uint32_t w0 = tid; w0 < totw; w0 += nt * UW) {
-                uint32_t v0[UW], v1[UW], v2[UW], b[UW], r[UW];
+        // the scan's tiles of this thread (pads, count reset)
+        const uint32_t sper = (B + nt - 1) / nt, slo = min(B, tid * sper), shi = min(B, slo + sper);
+        for (uint32_t e_lo = 0;; e_lo += S) {
+            const uint32_t e_hi = min(tot, e_lo + S);
+            const bool last = e_hi == tot;
 #pragma unroll
-                for (int u = 0; u < UW; ++u) {
-                    const uint32_t e = 3 * min(w0 + u * nt, totw - 1);
-                    v0[u] = stage[e];
-                    v1[u] = stage[e + 1];
-                    v2[u] = stage[e + 2];
-                    b[u] = v0[u] >> tm.tb;
-                }
+            for (int u = 0; u < KPT; ++u) {
+                const uint32_t slot_key = u * nt + tid;
+                if (uint32_t(u) < kpt && s0 + slot_key < s1) {
 #pragma unroll
-                for (int u = 0; u < UW; ++u) r[u] = cb[b[u]] + 3 * (w0 + u * nt);
-                uint32_t over = 0;
-#pragma unroll
-                for (int u = 0; u < UW; ++u) {
-                    const bool live = w0 + u * nt < totw;
-                    const uint32_t a = v0[u] & lmask;
-                    const uint32_t c1 = (v1[u] >> tm.tb) == b[u] ? (v1[u] & lmask) : a;
-                    const uint32_t c2 = (v2[u] >> tm.tb) == b[u] ? (v2[u] & lmask) : a;
-                    const uint64_t word = uint64_t(a) | (uint64_t(c1) << kPk3Bits) | (uint64_t(c2) << (2 * kPk3Bits));
-                    if (live && r[u] < pg.cap) rgn64[__umul24(b[u], capw) + div3(r[u])] = word;
-                    over |= uint32_t(live && r[u] >= pg.cap) << u;
-                }
-                if (over) {  // region overflow: heavy key duplication only
-#pragma unroll
-                    for (int u = 0; u < UW; ++u) {
-                        if ((over >> u) & 1u) {
-                            const uint32_t x = atomicAdd(ovf_count, 3u);
-                            ovf[x] = v0[u];
-                            ovf[x + 1] = (v1[u] >> tm.tb) == b[u] ? v1[u] : v0[u];
-                            ovf[x + 2] = (v2[u] >> tm.tb) == b[u] ? v2[u] : v0[u];
+                    for (int s = 0; s < KMAX; ++s) {
+                        if (s < k) {
+                            const uint32_t p = pos[u * KMAX + s];
+                            const uint32_t slot = rank_of(u * KMAX + s) - e_lo;
+                            if (slot < S) {
+                                stage[slot] = PROBE ? (((gkey0 + slot_key) << kSlotShift) | (p & lmask)) : p;
+                                if constexpr (PROBE) bkt[slot] = uint16_t(p >> tm.tb);
+                            }
                         }
                     }
                 }
             }
-            continue;
-        }
-        for (uint32_t e0 = tid; e0 < tot; e0 += nt * UW) {
-            uint32_t v[UW], b[UW], r[UW];
-#pragma unroll
-            for (int u = 0; u < UW; ++u) {
-                const uint32_t e = min(e0 + u * nt, tot - 1);
-                v[u] = stage[e];
-                b[u] = PROBE ? uint32_t(bkt[e]) : (v[u] >> tm.tb);
+            for (uint32_t b = slo; b < shi; ++b) {
+                if constexpr (PK3) {
+                    // the run's 0-2 pad slots: a position of another tile ((b ^ 1) << tb)
+                    const uint32_t c = cnt[b], l0 = lbase[b];
+                    for (uint32_t y = c; y < padded(c); ++y)
+                        if (l0 + y - e_lo < S) stage[l0 + y - e_lo] = (b ^ 1u) << tm.tb;
+                }
+                if (last) cnt[b] = 0;
             }
-#pragma unroll
-            for (int u = 0; u < UW; ++u) r[u] = cb[b[u]] + e0 + u * nt;
-            uint32_t over = 0;
-#pragma unroll
-            for (int u = 0; u < UW; ++u) {
-                const bool live = e0 + u * nt < tot;
-                if (live && r[u] < pg.cap) rgn[__umul24(b[u], pg.cap) + r[u]] = v[u];
-                over |= uint32_t(live && r[u] >= pg.cap) << u;
+            lds_barrier();
+            // The next sub-chunk is hashed and counted while the last window is written out: the
+            // hash's VALU work overlaps the write-out's LDS reads and stores (other waves).
+            if (last && s1 < k1) {
+                hash_count(s1);
+                if (s1 + pg.kps < k1) load_keys(s1 + pg.kps);
             }
-            if (over) {  // region overflow: heavy key duplication only
+            // Lane-parallel write-out: window entry e goes to position cb[b] + e_lo + e of region
+            // (g, b).  UW entries per thread per batch: the stage reads, then the cursor reads, are
+            // issued before any is consumed (one LDS wait each), and the region offsets are 32-bit
+            // within the workgroup's regions (B * cap < 2^32; b < 4096, cap < 2^24: one 24-bit
+            // multiply-add).  Positions >= cap overflow (rare).
+            const uint32_t nw = e_hi - e_lo;
+            // (four per batch when the next sub-chunk's KPT x KMAX positions and ranks already hold
+            // 60 registers: C4's k = 10 build, which spills at eight)
+            constexpr int UW = KPT * KMAX >= 30 ? 4 : 8;
+            if constexpr (PK3) {
+                // one 8-byte word (three stage entries of one tile) per thread and batch slot
+                uint64_t* const rgn64 = reinterpret_cast<uint64_t*>(regions) + uint64_t(g) * B * (pg.cap / 3);
+                const uint32_t capw = pg.cap / 3, totw = nw / 3;
+                for (uint32_t w0 = tid; w0 < totw; w0 += nt * UW) {
+                    uint32_t v0[UW], v1[UW], v2[UW], b[UW], r[UW];
 #pragma unroll
-                for (int u = 0; u < UW; ++u) {
-                    if ((over >> u) & 1u) {
-                        if constexpr (PROBE)
-                            spill_probe(ps, pos_to_bit((b[u] << tm.tb) | (v[u] & lmask), tm),
-                                        s0 + ((v[u] >> kSlotShift) & (pg.kps - 1)));
-                        else
-                            ovf[atomicAdd(ovf_count, 1u)] = v[u];
+                    for (int u = 0; u < UW; ++u) {
+                        const uint32_t e = 3 * min(w0 + u * nt, totw - 1);
+                        v0[u] = stage[e];
+                        v1[u] = stage[e + 1];
+                        v2[u] = stage[e + 2];
+                        b[u] = v0[u] >> tm.tb;
+                    }
+#pragma unroll
+                    for (int u = 0; u < UW; ++u) r[u] = cb[b[u]] + e_lo + 3 * (w0 + u * nt);
+                    uint32_t over = 0;
+#pragma unroll
+                    for (int u = 0; u < UW; ++u) {
+                        const bool live = w0 + u * nt < totw;
+                        const uint32_t a = v0[u] & lmask;
+                        const uint32_t c1 = (v1[u] >> tm.tb) == b[u] ? (v1[u] & lmask) : a;
+                        const uint32_t c2 = (v2[u] >> tm.tb) == b[u] ? (v2[u] & lmask) : a;
+                        const uint64_t word = uint64_t(a) | (uint64_t(c1) << kPk3Bits) | (uint64_t(c2) << (2 * kPk3Bits));
+                        if (live && r[u] < pg.cap) rgn64[__umul24(b[u], capw) + div3(r[u])] = word;
+                        over |= uint32_t(live && r[u] >= pg.cap) << u;
+                    }
+                    if (over) {  // region overflow: heavy key duplication only
+#pragma unroll
+                        for (int u = 0; u < UW; ++u) {
+                            if ((over >> u) & 1u) {
+                                const uint32_t x = atomicAdd(ovf_count, 3u);
+                                ovf[x] = v0[u];
+                                ovf[x + 1] = (v1[u] >> tm.tb) == b[u] ? v1[u] : v0[u];
+                                ovf[x + 2] = (v2[u] >> tm.tb) == b[u] ? v2[u] : v0[u];
+                            }
+                        }
+                    }
+                }
+            } else {
+                for (uint32_t e0 = tid; e0 < nw; e0 += nt * UW) {
+                    uint32_t v[UW], b[UW], r[UW];
+#pragma unroll
+                    for (int u = 0; u < UW; ++u) {
+                        const uint32_t e = min(e0 + u * nt, nw - 1);
+                        v[u] = stage[e];
+                        b[u] = PROBE ? uint32_t(bkt[e]) : (v[u] >> tm.tb);
+                    }
+#pragma unroll
+                    for (int u = 0; u < UW; ++u) r[u] = cb[b[u]] + e_lo + e0 + u * nt;
+                    uint32_t over = 0;
+#pragma unroll
+                    for (int u = 0; u < UW; ++u) {
+                        const bool live = e0 + u * nt < nw;
+                        if (live && r[u] < pg.cap) rgn[__umul24(b[u], pg.cap) + r[u]] = v[u];
+                        over |= uint32_t(live && r[u] >= pg.cap) << u;
+                    }
+                    if (over) {  // region overflow: heavy key duplication only
+#pragma unroll
+                        for (int u = 0; u < UW; ++u) {
+                            if ((over >> u) & 1u) {
+                                if constexpr (PROBE)
+                                    spill_probe(ps, pos_to_bit((b[u] << tm.tb) | (v[u] & lmask), tm),
+                                                s0 + ((v[u] >> kSlotShift) & (pg.kps - 1)));
+                                else
+                                    ovf[atomicAdd(ovf_count, 1u)] = v[u];
+                            }
+                        }
                     }
                 }
             }
+            if (last) break;
+            lds_barrier();  // the window's stage reads are done before the next window is placed
         }
     }
     lds_barrier();

@@ -360,10 +360,16 @@ same = np.repeat(splitmix_hex_keys(22, 0, 1), 60000, axis=0)
 fx = PackedKeys.fixed(np.concatenate([distinct, same, distinct[:1000]]))
 d, off = varlen_keys(23, 0, 100000)
 vr = PackedKeys(d, 100000, offsets=off)
+# variable-length keys with one key repeated 60k times (the 4096-key sub-chunks' stage windows and
+# region overflow together)
+k0 = d[int(off[0]):int(off[1])]
+vd = PackedKeys(np.concatenate([d, np.tile(k0, 60000)]), 160000,
+                offsets=np.concatenate([off, off[-1] + np.uint64(len(k0)) * np.arange(1, 60001, dtype=np.uint64)]))
 probes = PackedKeys.fixed(np.concatenate([splitmix_hex_keys(21, 150000, 100000), same,
                                           np.repeat(splitmix_hex_keys(24, 0, 1), 50000, axis=0)]))
 # B = 1024 tiles (C2 geometry), 768 (non-power-of-two m), 16 (rings overflow constantly)
-for nb, pk, q in ((2 ** 27, fx, probes), (3 * 2 ** 25, vr, vr), (2 ** 21, fx, probes), (2 ** 27 + 12, vr, vr)):
+for nb, pk, q in ((2 ** 27, fx, probes), (3 * 2 ** 25, vr, vr), (2 ** 21, fx, probes), (2 ** 27 + 12, vr, vr),
+                  (2 ** 27, vd, vd)):
     want = o.build(nb, 6, pk, omp=True)
     want_hm = o.probe(want, 6, q, omp=True)
     bf = BloomFilter(nb, 6); bf.set_build_mode(2); bf.add_many(pk)
