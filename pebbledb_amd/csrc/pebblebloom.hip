@@ -597,13 +597,14 @@ struct PartPlan {
     uint32_t gtq;       // ring gather: quad-table bytes per tile (0 = binary search)
 };
 
-// Partition strategy: PBF_PART=sort|ring forces one (tests, measurements); default auto.
+// Partition strategy: PBF_PART=sort|ring|sort_build forces one (tests, measurements); default auto.
 int part_override() {
     static const int v = [] {
         const char* e = std::getenv("PBF_PART");
         if (!e) return 0;
         if (!std::strcmp(e, "sort")) return 1;
         if (!std::strcmp(e, "ring")) return 2;
+        if (!std::strcmp(e, "sort_build")) return 3;  // counting sort for builds only
         return 0;
     }();
     return v;
@@ -622,7 +623,7 @@ bool ring_pow2(const TileMap& tm) { return tm.im.mode == kPow2 && !tm.cspace; }
 // thread field), builds may take smaller sub-chunks (k = 10 over 1024 tiles: 512).
 uint32_t ring_kps(uint32_t B, uint32_t k, bool probe, uint32_t tb) {
     const int ov = part_override();
-    if (ov == 1 || k == 0 || k > 16 || B > 1024 || (probe && tb > kSlotShift)) return 0;
+    if (ov == 1 || (ov == 3 && !probe) || k == 0 || k > 16 || B > 1024 || (probe && tb > kSlotShift)) return 0;
     for (uint32_t kp = kRingKeysPerSub; kp >= (probe ? kRingKeysPerSub : 256u); kp /= 2)
         if (uint64_t(kp) * k * 4 <= uint64_t(B) * kRingEntries) return kp;
     return ov == 2 ? (probe ? kRingKeysPerSub : 256u) : 0u;
