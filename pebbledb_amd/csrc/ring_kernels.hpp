@@ -14,8 +14,8 @@
 //
 //   ring      32 entries per tile (RC), groups of GS = 16.  head = entries flushed (= the region
 //             write cursor, a multiple of GS), tail = entries appended; packed as the 16-bit
-//             halves of one u32 per tile.  Entry e of tile b sits at ring[b*RC + (e % RC)] and
-//             lands at region position e.
+//             halves of one u32 per tile.  Entry e of tile b sits at ring[b*RC + ((e + stagger(b))
+//             % RC)] and lands at region position e.
 //   sub-chunk kps keys (<= 1024, one per thread).  The host picks the geometry so a tile receives
 //             <= GS/2 positions per sub-chunk on average; a position that would overrun the ring
 //             (or the region capacity) leaves the stream into an LDS spill buffer, handled once at
@@ -51,6 +51,26 @@ constexpr uint32_t kRingDescPerWave = 128;  // flush descriptors per wave (64 ti
 // [B x RC], 16-B aligned, then the spill buffer (probe: 2 words per entry, build: 1).
 __host__ __device__ constexpr uint32_t ring_lds_base(uint32_t B) { return (B + 16 * kRingDescPerWave + 2 + 3) & ~3u; }
 __host__ __device__ constexpr uint32_t ring_lds_words(uint32_t B) { return ring_lds_base(B) + B * kRingEntries; }
+
+// Entry e of tile b sits at ring[b * RC + ((e + ring_stagger(b)) % RC)]: the appends of a
+// sub-chunk store to slots e that are close together in every tile (the tails advance alike), so
+// without the stagger their LDS banks ((b * RC + e) mod 32 = e mod 32) collide.  A multiple of 4,
+// so a flush group (4 entries from e, e a multiple of 4) stays one aligned 16-byte read.
+// (C2 0.680-0.681 vs 0.685 ms/step, C5 6.99 vs 7.20 ms: profiles/r04/s8/stagger_*.)
+__device__ __forceinline__ uint32_t ring_stagger(uint32_t b) {
+#if defined(PBF_RING_STAGGER32)
+    return b & 31u;
+#else
+    return (b & 7u) << 2;
+#endif
+}
+__device__ __forceinline__ uint4 ring_group4(const uint32_t* r, uint32_t e, uint32_t rmask) {
+#if defined(PBF_RING_STAGGER32)
+    return make_uint4(r[e & rmask], r[(e + 1) & rmask], r[(e + 2) & rmask], r[(e + 3) & rmask]);
+#else
+    return *reinterpret_cast<const uint4*>(r + (e & rmask));
+#endif
+}
 
 // Tile position of a hash when m is a power of two <= 2^32 (POW2) or in general.
 template <bool POW2>
@@ -186,7 +206,7 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
                         const uint32_t val = PROBE ? (tag | (p & lmask)) : p;
                         // every lane stores (a position that left the stream into the dump
                         // word): no per-seed exec-mask branch (build 0.196 -> 0.192 ms on C2)
-                        smem[ok ? ring_lds_base(B) + b * RC + (e & rmask) : dump] = val;
+                        smem[ok ? ring_lds_base(B) + b * RC + ((e + ring_stagger(b)) & rmask) : dump] = val;
                         spill |= uint32_t(!ok) << s;
                     }
                 }
@@ -228,7 +248,7 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
                         const uint32_t d = wd[gi];
                         const uint32_t tb = d & 0xFFFu;
                         const uint32_t e = (d >> 12) + q * 4;  // region position
-                        const uint4 v = *reinterpret_cast<const uint4*>(ring + tb * RC + (e & rmask));
+                        const uint4 v = ring_group4(ring + tb * RC, e + ring_stagger(tb), rmask);
                         st_stream<PROBE ? kNtProbePart : kNtBuildPart>(region_at(tb, e), v);
                     }
                 }
@@ -266,7 +286,7 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
                     const uint32_t d = wd[gi];
                     const uint32_t tb = d & 0xFFFu;
                     const uint32_t e = (d >> 12) + q * 4;
-                    const uint4 v = *reinterpret_cast<const uint4*>(ring + tb * RC + (e & rmask));
+                    const uint4 v = ring_group4(ring + tb * RC, e + ring_stagger(tb), rmask);
                     st_stream<PROBE ? kNtProbePart : kNtBuildPart>(region_at(tb, e), v);
                 }
             }
