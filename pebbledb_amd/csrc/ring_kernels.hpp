@@ -57,19 +57,11 @@ __host__ __device__ constexpr uint32_t ring_lds_words(uint32_t B) { return ring_
 // without the stagger their LDS banks ((b * RC + e) mod 32 = e mod 32) collide.  A multiple of 4,
 // so a flush group (4 entries from e, e a multiple of 4) stays one aligned 16-byte read.
 // (C2 0.680-0.681 vs 0.685 ms/step, C5 6.99 vs 7.20 ms: profiles/r04/s8/stagger_*.)
-__device__ __forceinline__ uint32_t ring_stagger(uint32_t b) {
-#if defined(PBF_RING_STAGGER32)
-    return b & 31u;
-#else
-    return (b & 7u) << 2;
-#endif
-}
+// (A 32-way stagger, b mod 32, with the flush reading 4 single entries: C2 0.700 vs 0.681-0.686,
+// C5 7.39 vs 6.98 ms; profiles/r04/s8/st32_*.)
+__device__ __forceinline__ uint32_t ring_stagger(uint32_t b) { return (b & 7u) << 2; }
 __device__ __forceinline__ uint4 ring_group4(const uint32_t* r, uint32_t e, uint32_t rmask) {
-#if defined(PBF_RING_STAGGER32)
-    return make_uint4(r[e & rmask], r[(e + 1) & rmask], r[(e + 2) & rmask], r[(e + 3) & rmask]);
-#else
     return *reinterpret_cast<const uint4*>(r + (e & rmask));
-#endif
 }
 
 // Tile position of a hash when m is a power of two <= 2^32 (POW2) or in general.

@@ -117,6 +117,28 @@ for step in "$@"; do
              traffic c4 --config c4 --steps 2 --warmup 1
              TRAFFIC_ARGS="--probe-scale 3.0" traffic c5 --config c5 --steps 2 --warmup 1 --no-host-c5 --no-compare ;;
     traffic_c5b) TRAFFIC_ARGS="--probe-scale 3.0" traffic c5 --config c5 --steps 2 --warmup 1 --no-host-c5 --no-compare ;;
+    traffic_all) traffic c2 --steps 5 --warmup 2
+             TRAFFIC_ARGS="--probe-scale 2.0" traffic c3 --config c3 --steps 2 --warmup 1
+             traffic c4 --config c4 --steps 2 --warmup 1
+             TRAFFIC_ARGS="--probe-scale 3.0" traffic c5 --config c5 --steps 2 --warmup 1 --no-host-c5 --no-compare ;;
+    final_1) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+             run pytest 900 python -u -m pytest tests -m gpu -x -v -rf --timeout 150 --timeout-method thread
+             run bench 600 python bench.py
+             prof prof 600 --steps 20 --warmup 5 --no-cpu-baseline --no-host-inclusive
+             run bench_c1 300 python bench.py --config c1 --steps 50 --warmup 5
+             PBF_SHARED_READERS=0 run bench_c1_excl 300 python bench.py --config c1 --steps 50 --warmup 5 ;;
+    final_2) run bench_c3 600 python bench.py --config c3 --steps 5 --warmup 2
+             run bench_c4 600 python bench.py --config c4 --steps 3 --warmup 1
+             run bench_c5 600 python bench.py --config c5 --steps 5 --warmup 2
+             run bench_c5mixed 600 python bench.py --config c5mixed --steps 5 --warmup 2
+             run bench_sst 600 python bench.py --config sst --steps 20 --warmup 3
+             prof prof_c3 600 --config c3 --steps 3 --warmup 1 --no-cpu-baseline --no-host-inclusive
+             PBF_STREAMS=1 prof prof_c4_serial 600 --config c4 --steps 2 --warmup 1 --no-cpu-baseline
+             prof prof_c5 600 --config c5 --steps 3 --warmup 1 --no-cpu-baseline --no-host-c5
+             export PBF_BENCH_DEVICE=0 PBF_BENCH_BACKEND=gloo
+             run sl_c2_n2 300 python bench.py --gpus 2 --steps 10 --warmup 3 --no-host-inclusive
+             run sl_c2_n4 300 python bench.py --gpus 4 --steps 10 --warmup 3 --no-host-inclusive
+             unset PBF_BENCH_DEVICE PBF_BENCH_BACKEND ;;
     final_c) run bench_c1 300 python bench.py --config c1 --steps 50 --warmup 5
              PBF_SHARED_READERS=0 run bench_c1_excl 300 python bench.py --config c1 --steps 50 --warmup 5
              run bench_c3 600 python bench.py --config c3 --steps 5 --warmup 2
