@@ -343,7 +343,7 @@ class BloomFilter:
 
     @property
     def last_build_detail(self) -> int:
-        """PBF_DETAIL_RING/SORT | (keys per sub-chunk / 256) << 12."""
+        """PBF_DETAIL_RING/SORT [| PBF_DETAIL_PACKED] | (keys per sub-chunk / 256) << 12."""
         return 0 if self._h is None else int(_native.lib().pbf_last_build_detail(self._h))
 
     @property
