@@ -37,3 +37,17 @@ def test_every_profiled_pass_kernel_is_assigned():
         if any(n.split("::")[1].startswith(p) for p in NOT_IN_A_PASS):
             continue
         assert pass_of(n) in ("build", "probe"), n
+
+
+def test_committed_traffic_matches_the_sources():
+    """bench.py fills roofline.traffic only from a PMC summary taken on the current kernel sources
+    (source digest); every committed config summary must be one (a kernel edit without new PMC
+    passes would leave the driver's bench line with traffic null)."""
+    import json
+
+    from pebbledb_amd.build import source_digest
+    for cfg in ("c2", "c3", "c4", "c5"):
+        t = json.load(open(os.path.join(REPO, "profiles", f"traffic_{cfg}.json")))
+        assert t["source_sha256"] == source_digest(), cfg
+        assert t["passes"]["build"]["traffic_bytes"] > 0 and t["passes"]["probe"]["traffic_bytes"] > 0
+    assert pass_of("pbf::k_tile_build<true>") == "build"
