@@ -63,7 +63,76 @@ def parse():
                     help="c5: skip the per-filter comparison leg (PMC passes of the fused probe alone)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher / rendezvous check only (gloo, no GPU work, no measurement)")
+    ap.add_argument("--c5-layout", default="keys", choices=["keys", "filters"],
+                    help="c5 over N ranks: 'keys' = every rank holds the 8 filters and probes 1/N of the batch "
+                         "through the fused path; 'filters' = 8/N filters per rank, the whole batch each")
+    ap.add_argument("--sim-world", type=int, default=1,
+                    help="c4/c5 on one GPU: run rank --sim-rank's share of a --sim-world-rank job (its filters, "
+                         "its keys), no process group; the JSON reports that rank's rate")
+    ap.add_argument("--sim-rank", type=int, default=0)
     return ap.parse_args()
+
+
+def rank_plan(config: str, world: int, rank: int, local: int, c4_keys: int = 125_000_000,
+              c5_probes: int = 100_000_000, c5_layout: str = "keys") -> dict:
+    """What rank `rank` of `world` does (no GPU needed; tests/test_bench_launch_cpu.py checks the
+    8-rank plans): its device (LOCAL_RANK), its filters and key ranges.
+
+    c2 / c3: one filter per rank over the rank's own keys (weak scaling).
+    c4: filters_for_rank(8, world, rank); filter g is built from keys [g*K, (g+1)*K) (K = 125M:
+        1B keys over the 8 filters, shard.key_range).
+    c5: 'keys' layout — every rank holds all 8 filters (1 GiB of bitmaps) and probes its 1/world
+        slice of the 100M-key batch (whole 64-key hit-mask words) through the fused multi-filter
+        path; 'filters' layout — filters_for_rank(8, world, rank) against the whole batch.  No
+        collective in either: the slices / filters are independent."""
+    from pebbledb_amd.shard import filters_for_rank, key_range
+    plan = {"rank": rank, "world": world, "device": local}
+    if config == "c4":
+        fl = filters_for_rank(8, world, rank)
+        plan.update(filters=fl, key_ranges={g: key_range(g, c4_keys) for g in fl})
+    elif config == "c5":
+        if c5_layout == "keys":
+            words = (c5_probes + 63) // 64
+            a = min(c5_probes, (words * rank // world) * 64)
+            b = min(c5_probes, (words * (rank + 1) // world) * 64)
+            plan.update(filters=list(range(8)), probe_keys=(a, b), layout="keys")
+        else:
+            plan.update(filters=filters_for_rank(8, world, rank), probe_keys=(0, c5_probes), layout="filters")
+    else:
+        plan.update(filters=[rank])
+    return plan
+
+
+def c5_probe_key_spans(nq: int, n_f: int, a: int, b: int):
+    """The generator spans of probe keys [a, b) of C5's batch: (dst index, splitmix start, count).
+    Keys [0, nq/2) are members, 1/8 from each filter's key range; the rest are absent keys
+    (splitmix indices from 8 * n_f)."""
+    half = nq // 2
+    per = half // 8
+    spans = []
+    for g in range(8):
+        lo, hi = g * per, (g * per + (per if g < 7 else half - 7 * per))
+        x, y = max(a, lo), min(b, hi)
+        if x < y:
+            spans.append((x - a, g * n_f + (x - lo), y - x))
+    x, y = max(a, half), b
+    if x < y:
+        spans.append((x - a, 8 * n_f + (x - half), y - x))
+    return spans
+
+
+def init_process_group_or_exit(dist, torch, backend: str, local: int, rank: int) -> None:
+    """The timing's process group.  RCCL ('nccl') must come up or the run fails with exit code 3
+    (never silently timed over another backend); gloo only when asked for (the one-GPU rehearsal)."""
+    if backend == "nccl":
+        try:
+            dist.init_process_group(backend="nccl", init_method="env://", device_id=torch.device("cuda", local))
+        except Exception as e:  # noqa: BLE001 - reported, then a non-zero exit
+            print(f"rank {rank}: RCCL process group failed ({e!r}); set PBF_BENCH_BACKEND=gloo for a "
+                  f"gloo-timed rehearsal", file=sys.stderr)
+            sys.exit(3)
+    else:
+        dist.init_process_group(backend=backend, init_method="env://")
 
 
 def algorithmic_bytes(n, L, k, m_bits, offsets):
@@ -391,7 +460,12 @@ def sets_main(args, rank, world, local, torch, dist, np):
 
     set_default_device(local)
     L = _native.lib()
-    mine = filters_for_rank(8, world, rank)
+    # the rank's share (rank_plan); --sim-world W --sim-rank R runs rank R's share of a W-rank job
+    # on this one GPU, without a process group
+    sim = args.sim_world > 1
+    plan = rank_plan(args.config, args.sim_world if sim else world, args.sim_rank if sim else rank, local,
+                     args.c4_keys, args.c5_probes, args.c5_layout)
+    mine = plan["filters"]
     if args.config == "c4":
         n = args.c4_keys
         p = 0.001
@@ -415,11 +489,13 @@ def sets_main(args, rank, world, local, torch, dist, np):
                 bf.add_device_fixed(keys[g].data_ptr(), 16, n)
                 if ev is not None:
                     ev[i][1].record(torch.cuda.ExternalStream(bf.stream))
-        unit_total = n * 8  # every rank builds its share of the 8 filters per step
+        unit_total = n * (len(mine) if sim else 8)  # every rank builds its share of the 8 filters per step
     else:
         n_f = 10_000_000
         nb_bytes, k = 2 ** 27, 6
-        nq = args.c5_probes
+        nq_all = args.c5_probes
+        qa, qb = plan["probe_keys"]  # this rank's slice of the batch
+        nq = qb - qa
         filters = {}
         kb = torch.empty(n_f * 16, dtype=torch.uint8, device="cuda")
         for g in mine:
@@ -430,13 +506,12 @@ def sets_main(args, rank, world, local, torch, dist, np):
             bf.sync()
             filters[g] = bf
         del kb
-        q = torch.empty(nq * 16, dtype=torch.uint8, device="cuda")
-        half = nq // 2
+        q = torch.empty(max(nq, 1) * 16, dtype=torch.uint8, device="cuda")
+        half = nq_all // 2
         per = half // 8
-        for g in range(8):  # members: 1/8 of the half from each filter's range
-            cnt = per if g < 7 else half - 7 * per
-            _native.check(L.pbf_gen_splitmix_hex(local, None, q.data_ptr() + g * per * 16, SEED, g * n_f, cnt), "gen")
-        _native.check(L.pbf_gen_splitmix_hex(local, None, q.data_ptr() + half * 16, SEED, 8 * n_f, nq - half), "gen")
+        # members: 1/8 of the batch's first half from each filter's range; then absent keys
+        for dst, start, cnt in c5_probe_key_spans(nq_all, n_f, qa, qb):
+            _native.check(L.pbf_gen_splitmix_hex(local, None, q.data_ptr() + dst * 16, SEED, start, cnt), "gen")
         hms = {g: torch.zeros((nq + 7) // 8, dtype=torch.uint8, device="cuda") for g in mine}
         fl = [filters[g] for g in mine]
         s0 = fl[0]
@@ -449,7 +524,8 @@ def sets_main(args, rank, world, local, torch, dist, np):
             probe_multi_device(fl, q.data_ptr(), nq, [hms[g].data_ptr() for g in mine], key_len=16)
             if ev is not None:
                 ev[0][1].record(stream)
-        unit_total = nq * 8  # key x filter probes per step over all ranks
+        # key x filter probes per step over all ranks (a simulated rank: its own share)
+        unit_total = nq * len(mine) if sim else nq_all * 8
 
     nev = len(mine) if args.config == "c4" else 1
     events = [[[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(nev)] for _ in range(args.steps)]
@@ -487,14 +563,17 @@ def sets_main(args, rank, world, local, torch, dist, np):
         fp_rate = float(np.unpackbits(hm2.cpu().numpy()).sum()) / 1e6
     else:
         fp_total, fp_expect = 0, 0.0
+        n_abs = max(0, qb - max(qa, half))  # the rank's absent keys
         for g in mine:
             bits = np.unpackbits(hms[g].cpu().numpy(), bitorder="little")[:nq]
             cnt = per if g < 7 else half - 7 * per
-            ok &= bool(bits[g * per:g * per + cnt].all())
-            # the absent half: false positives at the filter's own rate (fill^k)
+            lo, hi = max(qa, g * per), min(qb, g * per + cnt)  # g's members in the rank's slice
+            if lo < hi:
+                ok &= bool(bits[lo - qa:hi - qa].all())
+            # the absent keys: false positives at the filter's own rate (fill^k)
             fill = filters[g].popcount() / (8 * nb_bytes)
-            fp_total += int(bits[half:].sum())
-            fp_expect += (nq - half) * fill ** k
+            fp_total += int(bits[nq - n_abs:].sum())
+            fp_expect += n_abs * fill ** k
         fp_ok = fp_total <= 3 * fp_expect + 20 * len(mine)
     host_c5 = None
     if args.config == "c5" and not args.no_host_c5:
@@ -502,6 +581,8 @@ def sets_main(args, rank, world, local, torch, dist, np):
     if world > 1:
         elapsed = float(all_reduce_scalar(torch, dist, elapsed, dist.ReduceOp.MAX, torch.float64))
         ok = bool(all_reduce_scalar(torch, dist, 1 if ok else 0, dist.ReduceOp.MIN, torch.int32))
+        if args.config == "c5":
+            fp_ok = bool(all_reduce_scalar(torch, dist, 1 if fp_ok else 0, dist.ReduceOp.MIN, torch.int32))
     if rank == 0:
         ms = elapsed / args.steps * 1e3
         if args.config == "c4":
@@ -515,9 +596,10 @@ def sets_main(args, rank, world, local, torch, dist, np):
             # then costs its k 4-B bitmap reads per key and its hit mask (SURVEY.md §8d probe
             # bytes, key term counted once): nq*L + nf*(4*nq*k + nq/8)
             b_pass = nq * 16 + len(mine) * (4 * nq * k + nq // 8)
-            metric, unit = f"Mprobes/s (key x filter) batched probe, {nq // 1_000_000}M keys vs 8x128MiB filters", "Mprobes/s"
-            what = (f"c5: {nq} probe keys (half members) x 8 filters (nb_bytes=2^27, k=6, 10M keys each); "
-                    f"a step = one pbf_probe_multi over the rank's {len(mine)} filters")
+            metric, unit = f"Mprobes/s (key x filter) batched probe, {nq_all // 1_000_000}M keys vs 8x128MiB filters", "Mprobes/s"
+            what = (f"c5: {nq_all} probe keys (half members) x 8 filters (nb_bytes=2^27, k=6, 10M keys each); "
+                    f"layout '{plan['layout']}': the rank probes keys [{qa}, {qb}) against its {len(mine)} filters "
+                    f"in one pbf_probe_multi per step")
             pk = ("multi-filter probe (shared k_part_ring + one XCD-aware k_tile_probe_set over every filter + "
                   "one fused k_gather_ring<8>)")
         if args.config == "c4":
@@ -530,7 +612,7 @@ def sets_main(args, rank, world, local, torch, dist, np):
         # rank's filters; profiles/traffic_c5.json: the multi-filter probe, already x its pipelines)
         tr = measured_traffic(args.config)
         traffic = None
-        if tr is not None:
+        if tr is not None and (args.config == "c4" or nq == nq_all):  # (measured on the whole batch)
             traffic = int(tr["build"] * len(mine)) if args.config == "c4" else int(tr["probe"])
         out = {
             "metric": metric, "value": round(unit_total / (ms * 1e-3) / 1e6, 3),
@@ -538,7 +620,8 @@ def sets_main(args, rank, world, local, torch, dist, np):
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u32",
             "data": "synthetic (splitmix64 hex keys generated on device)",
             "config": {"workload": what, "nb_bytes": nb_bytes, "k": k, "filters_per_rank": len(mine),
-                       "parallelism": f"filters-over-gpus x{world}"},
+                       "parallelism": (f"keys-over-gpus x{world}" if args.config == "c5" and plan.get("layout") == "keys"
+                                       else f"filters-over-gpus x{world}")},
             "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": pk,
                          "algorithmic_bytes": int(b_pass), "avg_ms": round(pass_ms, 4),
@@ -546,6 +629,10 @@ def sets_main(args, rank, world, local, torch, dist, np):
             "check": {"members_all_hit": ok},
             **dist_report(dist, world),
         }
+        if sim:
+            out["simulated_rank"] = {"rank": args.sim_rank, "world": args.sim_world,
+                                     "note": "one rank's share of a --sim-world job on this GPU; value = that "
+                                             "rank's units / its time (no process group)"}
         if fp_rate is not None:
             out["check"]["fp_rate_1M_absent"] = fp_rate
         if args.config == "c5":
@@ -914,10 +1001,17 @@ def dry_run(args, rank, world, dist):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
         seen = dist.get_world_size()
+    # every rank's placement as its own process computed it (LOCAL_RANK -> device, filters, keys)
+    plan = rank_plan(args.config, world, rank, int(os.environ.get("LOCAL_RANK", "0")), args.c4_keys,
+                     args.c5_probes, args.c5_layout)
+    plans = [plan]
+    if world > 1:
+        plans = [None] * world
+        dist.all_gather_object(plans, plan)
     if rank == 0:
         print(json.dumps({"dry_run": True, "metric": None, "value": None, "n_gpus": world, "world_size_seen": seen,
                           "backend": "gloo" if world > 1 else None, "max_elapsed_s": round(elapsed, 4),
-                          "config": {"workload": args.config}}), flush=True)
+                          "config": {"workload": args.config}, "plans": plans}), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
@@ -953,16 +1047,7 @@ def main():
         # collective.  If RCCL cannot start the run fails (exit 3) rather than
         # silently timing over another backend; gloo only when asked for (PBF_BENCH_BACKEND=gloo,
         # the one-GPU rehearsal).
-        backend = os.environ.get("PBF_BENCH_BACKEND", "nccl")
-        if backend == "nccl":
-            try:
-                dist.init_process_group(backend="nccl", init_method="env://", device_id=torch.device("cuda", local))
-            except Exception as e:  # noqa: BLE001 - reported, then a non-zero exit
-                print(f"rank {rank}: RCCL process group failed ({e!r}); set PBF_BENCH_BACKEND=gloo for a "
-                      f"gloo-timed rehearsal", file=sys.stderr)
-                sys.exit(3)
-        else:
-            dist.init_process_group(backend=backend, init_method="env://")
+        init_process_group_or_exit(dist, torch, os.environ.get("PBF_BENCH_BACKEND", "nccl"), local, rank)
 
     if args.config == "c5mixed":
         mixed_main(args, rank, world, local, torch, dist, np)

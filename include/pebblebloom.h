@@ -125,6 +125,14 @@ int pbf_probe_multi_placed(pbf_filter_t* const* filters, uint32_t nfilters, cons
                            const uint8_t* keys, const uint64_t* offsets, uint32_t key_len, uint64_t n,
                            uint8_t* const* hitmasks);
 
+/* The placement step of pbf_probe_multi_placed (and of a host-batch pbf_probe_multi over
+ * filters on several devices, grouped by device), as a pure function that runs without a GPU:
+ * slot_of[i] = filter i's group in first-appearance order of group_of (the order the groups'
+ * host threads start), *ngroups = the number of groups.  PBF_ERR_INVALID when two filters of
+ * one group name different devices (device_of[i] = filter i's device). */
+int pbf_plan_groups(const uint32_t* group_of, const int32_t* device_of, uint32_t n, uint32_t* slot_of,
+                    uint32_t* ngroups);
+
 /* BloomFilter.may_contain(key) for ONE key (bloom_filter.py:67-74), the per-key call of
  * LsmStorage.get (lsm_storage.py:165,175): key is host memory (UTF-8 bytes, len may be 0),
  * *out = 1 or 0.  Synchronous; the key goes to the kernel through mapped pinned memory and the
@@ -260,7 +268,8 @@ int pbf_plan_blocks(const uint64_t* key_offsets, const uint64_t* value_offsets, 
  * one), the last builder kept only if its position is past 0.  Outputs for pbf_build_sstables:
  * block_first / block_out (n+1 entries each; block_out laid end to end over the tables' data
  * sections), table_blocks (n+1 entries; table t = blocks [table_blocks[t], table_blocks[t+1])),
- * the counts, and the records covered (*written <= n). */
+ * the counts, and the records covered (*written <= n).  max_sstable_size 0 is refused
+ * (PBF_ERR_INVALID). */
 int pbf_plan_compaction(const uint64_t* key_offsets, const uint64_t* value_offsets, uint64_t n, uint64_t block_size,
                         uint64_t max_sstable_size, uint64_t* block_first, uint64_t* block_out, uint64_t* table_blocks,
                         uint64_t* nblocks, uint64_t* ntables, uint64_t* written);

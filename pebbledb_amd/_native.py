@@ -43,6 +43,7 @@ SIGNATURES = {
     "pbf_probe_multi_fixed": (_int, [_vp, _u32, _u8p, _u32, _u64, _vp, _int]),
     "pbf_probe_multi": (_int, [_vp, _u32, _u8p, _vp, _u64, _vp, _int]),
     "pbf_probe_multi_placed": (_int, [_vp, _u32, _vp, _u8p, _vp, _u32, _u64, _vp]),
+    "pbf_plan_groups": (_int, [_vp, _vp, _u32, _vp, _vp]),
     "pbf_hash_indices_fixed": (_int, [_vp, _u8p, _u32, _u64, _vp, _int]),
     "pbf_hash_indices": (_int, [_vp, _u8p, _vp, _u64, _vp, _int]),
     "pbf_get_bitmap": (_int, [_vp, _u8p, _u64]),

@@ -674,8 +674,8 @@ PartPlan plan_ring(uint32_t B, uint32_t k, uint64_t n, uint32_t kps, bool probe,
     pl.pg.cap = uint32_t(((cap + 31) / 32) * 32);
     // the rest of the CU's 160 KiB of LDS (up to 4096 entries) buffers spilled positions
     const size_t ring_bytes = size_t(ring_lds_words(B)) * 4, spill_entry = probe ? 8 : 4;
-    pl.pg.spill_cap = uint32_t(std::min<size_t>(4096, (160 * 1024 - ring_bytes) / spill_entry));
-    pl.lds_part = ring_bytes + size_t(pl.pg.spill_cap) * spill_entry;
+    pl.pg.spill_cap = uint32_t(std::min<size_t>(4096, (size_t(kRingLdsWords) * 4 - ring_bytes) / spill_entry));
+    pl.lds_part = 0;  // k_part_ring declares the CU's whole LDS statically (kRingLdsWords)
     set_gather(pl, B, pl.pg.nq + 1, nf);
     return pl;
 }
@@ -766,9 +766,9 @@ PartPlan plan_for(const TileMap& tm, uint32_t k, int km, uint64_t n, bool probe,
     const double share = busiest_tile_share(tm);
     if (const uint32_t kps = ring_kps(B, k, probe, tm.tb)) {
         const PartPlan pl = plan_ring(B, k, n, kps, probe, share, probe ? nf : 1);
-        // head / tail are 16-bit halves in LDS (cap <= 32768); entry offsets within a
+        // lim / tail are 16-bit byte counts in LDS (cap <= kRingMaxCap); entry offsets within a
         // workgroup's regions are 32-bit (B * cap < 2^32)
-        if (pl.pg.cap <= 32768 && uint64_t(B) * pl.pg.cap < (uint64_t(1) << 32)) return pl;
+        if (pl.pg.cap <= kRingMaxCap && uint64_t(B) * pl.pg.cap < (uint64_t(1) << 32)) return pl;
     }
     return plan_partition(B, k, km, n, probe, share, probe ? nf : 1);
 }
@@ -822,7 +822,8 @@ int run_tiled(pbf_filter_t* f, const Batch& b) {
     const uint32_t k = f->k;
     const PartPlan pl = plan_for(tm, k, b.km, b.n, false);
     const PartGeom& pg = pl.pg;
-    HIP_TRY(f->sc->regions.ensure(size_t(pg.G) * B * pg.cap * 4));
+    // (+ the ring partition's 64-B dummy line per workgroup after the regions)
+    HIP_TRY(f->sc->regions.ensure(size_t(pg.G) * B * pg.cap * 4 + size_t(pg.G) * 64));
     HIP_TRY(f->sc->fill.ensure(size_t(pg.G) * B * 4));
     HIP_TRY(f->sc->ovf.ensure(std::max<uint64_t>(b.n * k, 1) * 4));
     HIP_TRY(f->sc->ovf_count.ensure(64));
@@ -893,7 +894,7 @@ int run_tiled_probe_set(pbf_filter_t* f, pbf_filter_t* const* fs, uint32_t nf, c
     const PartPlan pl = plan_for(tm, k, b.km, b.n, true, nf);
     const PartGeom& pg = pl.pg;
     f->last_probe_detail = (pg.ring ? PBF_DETAIL_RING : PBF_DETAIL_SORT) | (nf << 8);
-    HIP_TRY(sc->regions.ensure(size_t(pg.G) * B * pg.cap * 4));
+    HIP_TRY(sc->regions.ensure(size_t(pg.G) * B * pg.cap * 4 + size_t(pg.G) * 64));
     HIP_TRY(sc->fill.ensure(size_t(pg.G) * B * 4));
     // both partitions: in-region counts at every 4096-key group boundary
     HIP_TRY(sc->pref.ensure(size_t(pg.G) * B * (pg.nq + 1) * 2));  // u16 (cap < 2^16)
@@ -1394,14 +1395,15 @@ int check_keys(pbf_filter_t* f, const uint8_t* keys, const uint64_t* offsets, ui
 // wait costs a host core almost nothing and does not depend on an interrupt-driven wake-up
 // (PBF_SPIN_US sets the pure polling budget, default 200 us).
 //
-// A wait has a deadline (PBF_WAIT_S seconds, default 60 — no call of this library runs for
-// more than a fraction of a second of GPU time; the GPU box's own silence limit is 3 minutes):
-// past it the call fails with PBF_ERR_HIP naming the stream and the last kernel enqueued on it,
-// instead of spinning silently.  (Round 2 saw one GPU-suite run hang inside a wait that blocked
-// on an event created with hipEventBlockingSync, i.e. on an interrupt-driven wake-up; no log of
-// the run was kept.  Every kernel's loops are bounded and its barriers uniform, and since the
-// blocking wait was replaced by polling no run has hung — but that is not proof, so the wait now
-// reports a stream that does not finish: DESIGN.md §1.)
+// A wait has a reporting deadline (PBF_WAIT_S seconds, default 60 — no call of this library
+// runs for more than a fraction of a second of GPU time; the GPU box's own silence limit is 3
+// minutes): past it the wait prints the stream and the last kernel enqueued on it to stderr, then
+// blocks until the stream is idle (queued copies may still target host memory the caller owns,
+// and the leased scratch must not be reused under running kernels) and the call returns
+// PBF_ERR_HIP.  A stream that never finishes is therefore reported, not returned from: the
+// deadline is a diagnostic, not a bound.  (Round 2 saw one GPU-suite run hang inside a wait that
+// blocked on an event created with hipEventBlockingSync, an interrupt-driven wake-up; since the
+// polling wait replaced it no run has hung: DESIGN.md §1.)
 int wait_raw(hipStream_t stream, int device, const char* last_kernel) {
     static const long spin_us = [] {
         const char* e = std::getenv("PBF_SPIN_US");
@@ -1542,22 +1544,24 @@ int probe_multi_impl(pbf_filter_t* const* fs, uint32_t nf, const uint8_t* keys, 
 // get order).  The calling thread runs the first group.  Host keys and hit masks only.
 int probe_multi_groups(pbf_filter_t* const* fs, uint32_t nf, const uint32_t* group_of, const uint8_t* keys,
                        const uint64_t* offsets, uint32_t key_len, uint64_t n, uint8_t* const* hitmasks) {
-    std::vector<uint32_t> ids;  // distinct groups in first-appearance order
+    std::vector<int32_t> dev(nf);
     for (uint32_t i = 0; i < nf; ++i) {
         if (!fs[i]) return fail(PBF_ERR_INVALID, "null filter handle in set");
         for (uint32_t j = 0; j < i; ++j)
             if (fs[j] == fs[i]) return fail(PBF_ERR_INVALID, "a filter appears twice in the set");
-        if (std::find(ids.begin(), ids.end(), group_of[i]) == ids.end()) ids.push_back(group_of[i]);
+        dev[i] = fs[i]->device;
     }
-    const size_t G = ids.size();
+    std::vector<uint32_t> slot(nf);
+    uint32_t ng = 0;
+    if (int rc = pbf_plan_groups(group_of, dev.data(), nf, slot.data(), &ng)) return rc;
+    const size_t G = ng;
+    std::vector<uint32_t> ids(G);  // group ids, first-appearance order
     std::vector<std::vector<pbf_filter_t*>> gfs(G);
     std::vector<std::vector<uint8_t*>> ghm(G);
     for (uint32_t i = 0; i < nf; ++i) {
-        const size_t g = size_t(std::find(ids.begin(), ids.end(), group_of[i]) - ids.begin());
-        if (!gfs[g].empty() && gfs[g][0]->device != fs[i]->device)
-            return fail(PBF_ERR_INVALID, "the filters of one placement group must share a device");
-        gfs[g].push_back(fs[i]);
-        ghm[g].push_back(hitmasks[i]);
+        ids[slot[i]] = group_of[i];
+        gfs[slot[i]].push_back(fs[i]);
+        ghm[slot[i]].push_back(hitmasks[i]);
     }
     std::vector<int> rcs(G, PBF_OK);
     std::vector<std::string> errs(G);
@@ -2147,6 +2151,25 @@ int pbf_probe_multi(pbf_filter_t* const* filters, uint32_t nfilters, const uint8
     return probe_multi_impl(filters, nfilters, kp, offsets, 0, n, hitmasks, on_device);
 }
 
+int pbf_plan_groups(const uint32_t* group_of, const int32_t* device_of, uint32_t n, uint32_t* slot_of,
+                    uint32_t* ngroups) {
+    if (n && (!group_of || !device_of || !slot_of)) return fail(PBF_ERR_INVALID, "null group, device or slot array");
+    std::vector<uint32_t> ids;   // distinct groups in first-appearance order
+    std::vector<int32_t> gdev;  // each group's device
+    for (uint32_t i = 0; i < n; ++i) {
+        const size_t g = size_t(std::find(ids.begin(), ids.end(), group_of[i]) - ids.begin());
+        if (g == ids.size()) {
+            ids.push_back(group_of[i]);
+            gdev.push_back(device_of[i]);
+        } else if (gdev[g] != device_of[i]) {
+            return fail(PBF_ERR_INVALID, "the filters of one placement group must share a device");
+        }
+        slot_of[i] = uint32_t(g);
+    }
+    if (ngroups) *ngroups = uint32_t(ids.size());
+    return PBF_OK;
+}
+
 int pbf_probe_multi_placed(pbf_filter_t* const* filters, uint32_t nfilters, const uint32_t* group_of,
                            const uint8_t* keys, const uint64_t* offsets, uint32_t key_len, uint64_t n,
                            uint8_t* const* hitmasks) {
@@ -2699,6 +2722,9 @@ int pbf_plan_compaction(const uint64_t* key_offsets, const uint64_t* value_offse
     if (!key_offsets || !value_offsets || !block_first || !block_out || !table_blocks || !nblocks || !ntables || !written)
         return fail(PBF_ERR_INVALID, "null pointer");
     if (block_size == 0 || block_size > kMaxBlockData) return fail(PBF_ERR_INVALID, "block_size must be in (0, 65536]");
+    // (the reference tests the position after every add, lsm_storage.py:241, so a size of 0 would
+    // make one table per record there; splitting where blocks finish agrees for any size > 0)
+    if (max_sstable_size == 0) return fail(PBF_ERR_INVALID, "max_sstable_size must be positive");
     // LsmStorage._compact (lsm_storage.py:233-251) over the greedy blocks of DataBlockBuilder.add
     // (blocks.py:78-95): a builder's position advances when a record does not fit the open block
     // (sstable.py:246-266); at position >= max_sstable_size the builder is built, its last block

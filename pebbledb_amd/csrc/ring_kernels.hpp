@@ -12,10 +12,13 @@
 // with ONE wave store instruction (4 lanes x 16 B), so each region line leaves as whole 64-B
 // requests.
 //
-//   ring      32 entries per tile (RC), groups of GS = 16.  head = entries flushed (= the region
-//             write cursor, a multiple of GS), tail = entries appended; packed as the 16-bit
-//             halves of one u32 per tile.  Entry e of tile b sits at ring[b*RC + ((e + stagger(b))
-//             % RC)] and lands at region position e.
+//   ring      32 entries per tile (RC), groups of GS = 16.  ht[b] = lim << 16 | tail, both in
+//             BYTES of region position (4 x entries): tail = entries appended to region (g, b),
+//             lim = min(head + RC, cap) with head = entries flushed (a multiple of GS).  Region
+//             entry e sits in ring slot e mod RC, so an append's LDS byte address is
+//             b * 128 + (tail & 124) and its overrun test one compare of the two halves (tail <
+//             lim); appends that fail it left the stream (spill below).  Thread b owns tile b in
+//             the flush and keeps head in a register.
 //   sub-chunk kps keys (<= 1024, one per thread).  The host picks the geometry so a tile receives
 //             <= GS/2 positions per sub-chunk on average; a position that would overrun the ring
 //             (or the region capacity) leaves the stream into an LDS spill buffer, handled once at
@@ -27,11 +30,13 @@
 //   probe     entry = key-in-group << 20 | position-in-tile, key-in-group = (j & 3) << 10 |
 //             thread (j = sub-chunk; a group = 4096 keys = 4 sub-chunks of 1024).  pref[g][q][b] = in-region entries
 //             of (g, b) before group q (b fastest, so a wave's stores of 64 tiles are one
-//             contiguous 256-B run), so k_gather_ring finds an entry's group from its region
+//             contiguous 128-B run), so k_gather_ring finds an entry's group from its region
 //             position.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include <type_traits>
 
 #include "tiled_kernels.hpp"
 
@@ -44,25 +49,37 @@ static_assert(kSlotShift == 20 && kRingKeysPerSub == 1024 && kGroupKeys == 4 * k
 // Key sub-chunks loaded per batch, one batch ahead: 2 measured best with the non-temporal streams
 // (C2 A/B over 1/2/3/4/8: profiles/r01/s11/ab.txt)
 constexpr int kRingPrefetch = 2;
-constexpr uint32_t kRingDescPerWave = 128;  // flush descriptors per wave (64 tiles x <= 2 groups)
+#ifndef PBF_DIAG_NOSTORE
+#define PBF_DIAG_NOSTORE 0
+#endif
+#ifndef PBF_DIAG_WMASK
+#define PBF_DIAG_WMASK 0xFFFFFFFFu
+#endif
+#ifndef PBF_DIAG_SINK
+#define PBF_DIAG_SINK 0
+#endif
+#ifndef PBF_DIAG_CONST
+#define PBF_DIAG_CONST 0
+#endif
+#ifndef PBF_DIAG_LOG
+#define PBF_DIAG_LOG 0
+#endif
+#ifndef PBF_DIAG_NOAPPEND
+#define PBF_DIAG_NOAPPEND 0
+#endif
+// Region capacity bound of the ring partition: tail (bytes) must stay below 2^16 although a
+// sub-chunk may append up to kps * k <= 8192 positions past lim (all to one tile: a duplicated
+// key) before the flush clamps it: 4 * (cap + 8192) < 2^16.
+constexpr uint32_t kRingMaxCap = 8160;
 
-// LDS layout of k_part_ring (u32 words): head|tail per tile [B], flush descriptors [16 waves x
-// 128], one dump word (appends that left the stream write there), the spill count, then the rings
-// [B x RC], 16-B aligned, then the spill buffer (probe: 2 words per entry, build: 1).
-__host__ __device__ constexpr uint32_t ring_lds_base(uint32_t B) { return (B + 16 * kRingDescPerWave + 2 + 3) & ~3u; }
-__host__ __device__ constexpr uint32_t ring_lds_words(uint32_t B) { return ring_lds_base(B) + B * kRingEntries; }
-
-// Entry e of tile b sits at ring[b * RC + ((e + ring_stagger(b)) % RC)]: the appends of a
-// sub-chunk store to slots e that are close together in every tile (the tails advance alike), so
-// without the stagger their LDS banks ((b * RC + e) mod 32 = e mod 32) collide.  A multiple of 4,
-// so a flush group (4 entries from e, e a multiple of 4) stays one aligned 16-byte read.
-// (C2 0.680-0.681 vs 0.685 ms/step, C5 6.99 vs 7.20 ms: profiles/r04/s8/stagger_*.)
-// (A 32-way stagger, b mod 32, with the flush reading 4 single entries: C2 0.700 vs 0.681-0.686,
-// C5 7.39 vs 6.98 ms; profiles/r04/s8/st32_*.)
-__device__ __forceinline__ uint32_t ring_stagger(uint32_t b) { return (b & 7u) << 2; }
-__device__ __forceinline__ uint4 ring_group4(const uint32_t* r, uint32_t e, uint32_t rmask) {
-    return *reinterpret_cast<const uint4*>(r + (e & rmask));
-}
+// LDS layout of k_part_ring, 4-byte words: ht[1024] (fixed, so the rings start at byte 4096 for
+// every B: the ring base is an instruction offset), the rings [B x RC], the dump word (appends
+// that left the stream store there), the spill count, two pad words, then the spill buffer
+// (probe: 2 words per entry, build: 1).
+constexpr uint32_t kRingHtWords = 1024;
+constexpr uint32_t kRingDescWords = 16 * 64 * 2;  // per wave 64 write-out descriptors of 8 B
+__host__ __device__ constexpr uint32_t ring_lds_words(uint32_t B) { return kRingHtWords + kRingDescWords + B * kRingEntries + 4; }
+constexpr uint32_t kRingLdsWords = 160 * 1024 / 4;  // declared statically by k_part_ring
 
 // Tile position of a hash when m is a power of two <= 2^32 (POW2) or in general.
 template <bool POW2>
@@ -76,43 +93,53 @@ __device__ __forceinline__ uint32_t ring_pos(uint32_t h, const TileMap& tm) {
 // batching pays that wait once per kRingPrefetch sub-chunks instead of once per sub-chunk.
 // EXACT: k == KMAX is known at compile time, so the per-seed `s < k` tests vanish and the k LDS
 // atomics of a key issue back to back.
-// The host keeps cap <= 32768, so a tail never passes cap + one sub-chunk's appends (the flush
-// clamps it every sub-chunk) and head / tail fit the 16-bit halves of one u32: the append is a
-// 32-bit LDS atomic spread over all 32 banks of a lane group.
+//
+// Per position the append is one LDS atomic (returns lim | tail), one compare, the slot address
+// (b << 7 | tail & 124, or the dump word) and one LDS store; per sub-chunk each thread flushes its
+// own tile: one LDS read of ht, and for a full group (16 entries) four 16-B LDS reads and four
+// 16-B stores to the region (the four stores of a group come from one lane in consecutive
+// instructions, so the L2 line is complete before it is written back).  (Round 4 listed the
+// complete groups of 64 tiles per wave with ballots and descriptors and wrote each group with
+// 4 lanes: ~45 VALU per thread and flush, against ~12 here.)
 template <int KMAX, int KM, bool PROBE, bool POW2, bool EXACT>
 __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k, TileMap tm, PartGeom pg,
                                                     uint32_t* __restrict__ regions, uint32_t* __restrict__ fill,
                                                     uint16_t* __restrict__ pref, uint32_t* __restrict__ ovf,
                                                     uint32_t* __restrict__ ovf_count, ProbeSet ps,
                                                     uint32_t* __restrict__ hw_init) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    // static LDS (the whole CU's 160 KiB): its base is a link-time constant, so the ring base
+    // and the region of an append fold into the LDS instructions' offsets
+    __shared__ __attribute__((aligned(16))) uint32_t smem[kRingLdsWords];
     if constexpr (EXACT) k = KMAX;
-    constexpr uint32_t RC = kRingEntries, GS = RC / 2, rmask = RC - 1;
+    constexpr uint32_t RC = kRingEntries;
     constexpr uint32_t SW = PROBE ? 2 : 1;  // spill-buffer words per entry
-    const uint32_t B = tm.nbuckets;
+#ifndef PBF_RING_PROBE_NT
+#define PBF_RING_PROBE_NT kNtProbePart
+#endif
+    constexpr bool NT = PROBE ? PBF_RING_PROBE_NT : kNtBuildPart;
+    const uint32_t B = tm.nbuckets;  // <= 1024 = blockDim.x (host: ring_kps)
     const uint32_t shift = tm.tb;
     const uint32_t kps = pg.kps;  // keys per sub-chunk (<= 1024 threads)
-    const uint32_t tid = threadIdx.x, nt = blockDim.x;
-    const uint32_t lane = tid & 63, wave = tid >> 6;
+    const uint32_t tid = threadIdx.x;
     const uint32_t g = blockIdx.x;
-    const uint32_t cap = pg.cap;
+    const uint32_t cap = pg.cap, cap4 = 4 * cap;  // cap <= kRingMaxCap (host)
     const uint32_t lmask = (1u << tm.tb) - 1u;
-    // ht[b] = head << 16 | tail: one LDS atomic add appends a position and returns the tile's
-    // flush cursor with its slot (no separate head read per position)
+    char* const lds = reinterpret_cast<char*>(smem);
+    constexpr uint32_t RING0 = (kRingHtWords + kRingDescWords) * 4;  // byte offset of the rings
     uint32_t* const ht = smem;
-    uint32_t* const desc = smem + B;                  // 16 waves x 128 group descriptors
-    const uint32_t dump = B + 16 * kRingDescPerWave;  // word index of the dump slot
+    const uint32_t dump = RING0 / 4 + B * RC;  // word index of the dump slot
     uint32_t* const nspill = smem + dump + 1;
-    uint32_t* const ring = smem + ring_lds_base(B);   // B * RC, 16-B aligned
-    uint32_t* const sbuf = ring + B * RC;             // pg.spill_cap entries
-    // this workgroup's regions; an entry's offset in them fits 32 bits (B * cap < 2^32), and
-    // tb < 4096, cap < 2^20 make it one 24-bit multiply-add
+    uint32_t* const sbuf = smem + dump + 4;  // pg.spill_cap entries
+    // the workgroup's regions; entry offsets within them fit 32 bits (B * cap < 2^32)
     uint32_t* const rgn = regions + uint64_t(g) * B * cap;
-    auto region_at = [&](uint32_t tb, uint32_t e) { return rgn + (__umul24(tb, cap) + e); };
     const uint32_t nqs = pg.nq + 1;  // pref entries per (g, b)
-    for (uint32_t b = tid; b < B; b += nt) {
-        ht[b] = 0;
-        if constexpr (PROBE) pref[uint64_t(g) * nqs * B + b] = 0;
+    // the flush: thread tid owns tile tid; its region write cursor (head, bytes) in a register
+    const bool owner = tid < B;
+    uint16_t* const own_pref = PROBE ? pref + uint64_t(g) * nqs * B + (owner ? tid : 0) : nullptr;  // [q * B]
+    uint32_t h4 = 0;
+    if (owner) {
+        ht[tid] = min(4u * RC, cap4) << 16;
+        if constexpr (PROBE) own_pref[0] = 0;
     }
     if (tid == 0) *nspill = 0;
     const uint64_t k0 = uint64_t(g) * pg.kpw;
@@ -120,7 +147,7 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
     if constexpr (PROBE) {
         // this workgroup's words of every filter's miss bits (neg) start at 0 and, when the
         // gather ANDs into words, every filter's gather words (hw_init) at all ones: no memsets
-        for (uint64_t w = (k0 >> 5) + tid; w < ((k1 + 31) >> 5); w += nt) {
+        for (uint64_t w = (k0 >> 5) + tid; w < ((k1 + 31) >> 5); w += blockDim.x) {
             for (uint32_t f = 0; f < ps.nf; ++f) {
                 ps.neg[f * ps.neg_stride + w] = 0u;
                 if (hw_init) hw_init[f * ps.neg_stride + w] = ~0u;
@@ -153,156 +180,203 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
             ovf[atomicAdd(ovf_count, 1u)] = p;
         }
     };
+    // Group write-out, dense store instructions: the wave lists the groups its 64 tiles write
+    // now (a ballot and a masked bit count give each its descriptor slot: ring byte offset,
+    // region byte offset), then each store instruction writes 16 of them, 4 lanes x 16 B per
+    // group, so a group leaves as one whole 64-B segment and the instruction is full.  (Each
+    // lane writing its own group as four 16-B stores: C2 probe partition 319 vs 251 us, four
+    // times the L2 write requests; quads writing their 4 tiles' groups in 4 DPP-broadcast rounds,
+    // whole segments but ~6 groups per store instruction: 271 vs 180 us without the stores.)
+    // Every call issues exactly two store instructions (32 groups; lanes past the last group
+    // rewrite it, the same bytes; with no group at all they write the workgroup's dummy line past
+    // the regions) and only a call with more than 32 groups a third: the compiler then counts the
+    // flush stores a key load is followed by, and the wait for the next keys lets those stores
+    // stay in flight instead of draining them (vmcnt counts loads and stores in issue order).
+    const uint32_t lane = tid & 63u, wave = tid >> 6;
+    uint2* const wdesc = reinterpret_cast<uint2*>(lds + kRingHtWords * 4) + wave * 64;
+    const uint32_t ring_own = tid << 7;   // ring byte offset of the owned tile
+    const uint32_t rgn_own = tid * cap4;  // its region's byte offset in the workgroup's regions (< 2^32)
+    const uint32_t q16 = (lane & 3u) << 4;
+    // the workgroup's 64-B dummy line after all regions (the host allocates G lines there)
+    const uint2 dummy = make_uint2(0u, uint32_t((uint64_t(pg.G) * B * cap - uint64_t(g) * B * cap) * 4 + g * 64));
+    // A flush's first 32 groups (two store instructions) are read from the rings into registers
+    // (take_groups) and stored after the next sub-chunk's hash (put_groups): the chain ht read ->
+    // descriptor write -> descriptor read -> ring read -> store no longer holds the wave between
+    // the barriers, its LDS latencies run under the hash.  Groups past 32 of a call are written
+    // at once (rare).
+    struct Pending {
+        uint4 x0, x1;    // pieces q of the wave's groups (lane >> 2) and 16 + (lane >> 2)
+        uint32_t a0, a1;  // their byte offsets in the workgroup's regions
+    };
+    auto take_groups = [&](bool has, uint32_t hb, Pending& pd) {  // wave-uniform
+        const uint64_t m = __builtin_amdgcn_ballot_w64(has);
+        const uint32_t total = uint32_t(__popcll(m));
+        if (has) {
+            const uint32_t slot = __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
+            wdesc[slot] = make_uint2(ring_own | (hb & 64u), rgn_own + hb);
+        }
+        __builtin_amdgcn_wave_barrier();
+        auto desc = [&](uint32_t c) { return total ? wdesc[min(c + (lane >> 2), total - 1)] : dummy; };
+        const uint2 d0 = desc(0), d1 = desc(16);
+        pd.x0 = *reinterpret_cast<const uint4*>(lds + RING0 + d0.x + q16);
+        pd.x1 = *reinterpret_cast<const uint4*>(lds + RING0 + d1.x + q16);
+        pd.a0 = d0.y + q16;
+        pd.a1 = d1.y + q16;
+        for (uint32_t c = 32; c < total; c += 16) {
+            const uint2 d = desc(c);
+            const uint4 x = *reinterpret_cast<const uint4*>(lds + RING0 + d.x + q16);
+            st_stream<NT>(reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(rgn) + (d.y + q16)), x);
+        }
+        __builtin_amdgcn_wave_barrier();
+    };
+    uint32_t diag_log = 0;
+    uint4 diag_x = make_uint4(0, 0, 0, 0);
+    auto put_groups = [&](const Pending& pd) {
+        if (PBF_DIAG_SINK) {  // diagnostic: no stores, the ring reads kept (their data folded into one word)
+            diag_x.x ^= pd.x0.x ^ pd.x1.y ^ pd.a0;
+            diag_x.y ^= pd.x0.y ^ pd.x1.z ^ pd.a1;
+            diag_x.z ^= pd.x0.z ^ pd.x1.w;
+            diag_x.w ^= pd.x0.w ^ pd.x1.x;
+        } else if (PBF_DIAG_CONST) {  // diagnostic: the stores without the ring reads' data
+            st_stream<NT>(reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(rgn) + pd.a0), make_uint4(pd.a0, 1, 2, 3));
+            st_stream<NT>(reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(rgn) + pd.a1), make_uint4(pd.a1, 1, 2, 3));
+        } else if (PBF_DIAG_LOG) {  // diagnostic: the same bytes as one contiguous log per wave
+            char* base = reinterpret_cast<char*>(rgn) + (uint32_t(wave) << 16);
+            st_stream<NT>(reinterpret_cast<uint32_t*>(base + ((diag_log & 0xFFFF) + lane * 16)), pd.x0);
+            st_stream<NT>(reinterpret_cast<uint32_t*>(base + (((diag_log + 1024) & 0xFFFF) + lane * 16)), pd.x1);
+            diag_log += 2048;
+        } else if (!PBF_DIAG_NOSTORE) {
+            st_stream<NT>(reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(rgn) + (pd.a0 & PBF_DIAG_WMASK)), pd.x0);
+            st_stream<NT>(reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(rgn) + (pd.a1 & PBF_DIAG_WMASK)), pd.x1);
+        }
+    };
+    auto write_groups = [&](bool has, uint32_t hb) {
+        Pending pd;
+        take_groups(has, hb, pd);
+        put_groups(pd);
+    };
+    uint32_t pos[KMAX];
+    auto hash_sub = [&](uint64_t s0, const uint4& w) {  // the positions of sub-chunk s0's key of this thread
+        const uint64_t i = s0 + tid;
+        if (tid < kps && i < k1) {
+            auto emit = [&](int s, uint32_t h) { pos[s] = ring_pos<POW2>(h, tm); };
+            if constexpr (F16)
+                murmur_seeds16<KMAX>(w, k, emit);
+            else
+                hash_key<KMAX, KM>(ks, i, k, emit);
+        }
+    };
+    // the first batch's keys are taken before the loop; inside it a batch's keys are taken at the
+    // end of the previous batch, after that batch's flush stores, which the wait lets stay in flight
     load_batch(k0);
+    uint4 cw[F16 ? P : 1];
+    if constexpr (F16) {
+#pragma unroll
+        for (int u = 0; u < P; ++u) cw[u] = kw[u];
+    }
+    hash_sub(k0, cw[0]);
     uint32_t j = 0;  // sub-chunks done
     for (uint64_t c0 = k0; c0 < k1; c0 += uint64_t(P) * kps) {
-        uint4 cw[F16 ? P : 1];
-        if constexpr (F16) {
-#pragma unroll
-            for (int u = 0; u < P; ++u) cw[u] = kw[u];
-        }
         if (c0 + uint64_t(P) * kps < k1) load_batch(c0 + uint64_t(P) * kps);
-#pragma unroll
-        for (int u = 0; u < P; ++u, ++j) {
+        // the batch's sub-chunks, u = 0 .. P-1 at compile time (cw[u] register-indexed)
+        auto sub = [&](auto U) {
+            constexpr int u = decltype(U)::value;
+            // (a batch's second sub-chunk past the workgroup's keys still runs, empty: every
+            // batch then issues the same stores, which the compiler's wait for the next keys counts)
             const uint64_t s0 = c0 + uint64_t(u) * kps;
-            if (s0 >= k1) break;
             const uint64_t i = s0 + tid;
             const bool live = tid < kps && i < k1;
-            uint32_t pos[KMAX], slot[KMAX], hd[KMAX];
-            // hash before the barrier: a wave done with its share of the previous flush hashes
-            // while the others still flush
-            if (live) {
-                auto emit = [&](int s, uint32_t h) { pos[s] = ring_pos<POW2>(h, tm); };
-                if constexpr (F16)
-                    murmur_seeds16<KMAX>(cw[u], k, emit);
-                else
-                    hash_key<KMAX, KM>(ks, i, k, emit);
-            }
-            lds_barrier();  // previous flush done: head / tail stable, rings free
-            if (live) {
+            lds_barrier();  // previous flush done: ht stable, rings free
+            if (!PBF_DIAG_NOAPPEND && live) {
+                uint32_t v[KMAX];
 #pragma unroll
-                for (int s = 0; s < KMAX; ++s) {
-                    if (s < k) {
-                        const uint32_t v = atomicAdd(ht + (pos[s] >> shift), 1u);
-                        slot[s] = v & 0xFFFFu;
-                        hd[s] = v >> 16;
-                    }
-                }
-                uint32_t spill = 0;  // positions that overrun their tile's ring or region
+                for (int s = 0; s < KMAX; ++s)
+                    if (s < k) v[s] = atomicAdd(ht + (pos[s] >> shift), 4u);
                 const uint32_t tag = PROBE ? (((j & 3u) << 30) | (tid << kSlotShift)) : 0u;
+                bool bad = false;  // a position overran its tile's ring or region
 #pragma unroll
                 for (int s = 0; s < KMAX; ++s) {
                     if (s < k) {
-                        const uint32_t p = pos[s], b = p >> shift, e = slot[s];
-                        const bool ok = e - hd[s] < RC && e < cap;
-                        const uint32_t val = PROBE ? (tag | (p & lmask)) : p;
-                        // every lane stores (a position that left the stream into the dump
-                        // word): no per-seed exec-mask branch (build 0.196 -> 0.192 ms on C2)
-                        smem[ok ? ring_lds_base(B) + b * RC + ((e + ring_stagger(b)) & rmask) : dump] = val;
-                        spill |= uint32_t(!ok) << s;
+                        const uint32_t b = pos[s] >> shift;
+                        const bool ok = (v[s] & 0xFFFFu) < (v[s] >> 16);
+                        // every lane stores (a position that left the stream into the dump word):
+                        // no per-seed exec-mask branch
+                        const uint32_t off = ok ? ((b << 7) | (v[s] & 124u)) : (dump * 4 - RING0);
+                        *reinterpret_cast<uint32_t*>(lds + RING0 + off) = PROBE ? (tag | (pos[s] & lmask)) : pos[s];
+                        bad |= !ok;
                     }
                 }
-                if (spill) {  // rare: heavy key duplication
+                if (bad) {  // rare: heavy key duplication
 #pragma unroll
                     for (int s = 0; s < KMAX; ++s)
-                        if ((spill >> s) & 1u) spill_one(pos[s], i);
+                        if (s < k && (v[s] & 0xFFFFu) >= (v[s] >> 16)) spill_one(pos[s], i);
                 }
             }
             lds_barrier();
-            // Flush: each wave owns 64 tiles per pass.  A lane's tile has 0..2 whole groups;
-            // the wave lists them (descriptor = tile | region position << 12) and writes
-            // 64/(GS/4) groups per store instruction, GS/4 lanes x 16 B per group, each whole.
-            uint32_t* wd = desc + wave * kRingDescPerWave;
-            constexpr uint32_t lpg = GS / 4;    // lanes per group
-            constexpr uint32_t gpi = 64 / lpg;  // groups per store instruction
-            for (uint32_t b0 = wave * 64; b0 < B; b0 += nt) {
-                const uint32_t b = b0 + lane;
-                uint32_t ng = 0, h = 0, t = 0;
-                if (b < B) {
-                    const uint32_t v = ht[b];
-                    h = v >> 16;
-                    t = min(v & 0xFFFFu, min(h + RC, cap));  // positions past these left the stream
-                    ng = (t - h) / GS;
+            // Flush: every tile's complete groups (<= 2) leave, the owner clamps its tail
+            Pending pd;
+            {
+                const uint32_t v = owner ? ht[tid] : 0u;
+                const uint32_t t4 = min(v & 0xFFFFu, v >> 16);  // positions past lim left the stream
+                bool more = h4 + 64 <= t4;
+                take_groups(more, h4, pd);  // always: its two stores on every path (put_groups below)
+                h4 += more ? 64u : 0u;
+                more = h4 + 64 <= t4;
+                while (__builtin_amdgcn_ballot_w64(more)) {  // wave-uniform: a second group is rare
+                    write_groups(more, h4);
+                    h4 += more ? 64u : 0u;
+                    more = h4 + 64 <= t4;
                 }
-                const uint64_t m1 = __ballot(ng >= 1), m2 = __ballot(ng >= 2);
-                // descriptors of lower lanes: masked bit counts (v_mbcnt), accumulated over m1, m2
-                const uint32_t at = __builtin_amdgcn_mbcnt_hi(
-                    uint32_t(m2 >> 32), __builtin_amdgcn_mbcnt_lo(
-                                            uint32_t(m2), __builtin_amdgcn_mbcnt_hi(
-                                                              uint32_t(m1 >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m1), 0u))));
-                const uint32_t total = __popcll(m1) + __popcll(m2);
-                if (ng >= 1) wd[at] = b | (h << 12);
-                if (ng >= 2) wd[at + 1] = b | ((h + GS) << 12);
-                __builtin_amdgcn_wave_barrier();
-                for (uint32_t c = 0; c < total; c += gpi) {
-                    const uint32_t gi = c + lane / lpg, q = lane % lpg;
-                    if (gi < total) {
-                        const uint32_t d = wd[gi];
-                        const uint32_t tb = d & 0xFFFu;
-                        const uint32_t e = (d >> 12) + q * 4;  // region position
-                        const uint4 v = ring_group4(ring + tb * RC, e + ring_stagger(tb), rmask);
-                        st_stream<PROBE ? kNtProbePart : kNtBuildPart>(region_at(tb, e), v);
-                    }
-                }
-                __builtin_amdgcn_wave_barrier();
-                if (b < B) {
-                    ht[b] = ((h + ng * GS) << 16) | t;
+                if (owner) {
+                    ht[tid] = (min(h4 + 4 * RC, cap4) << 16) | t4;
                     if constexpr (PROBE)
-                        if (((j + 1) & 3) == 0) pref[(uint64_t(g) * nqs + ((j + 1) >> 2)) * B + b] = uint16_t(t);
+                        if (((j + 1) & 3) == 0) own_pref[__umul24((j + 1) >> 2, B)] = uint16_t(t4 >> 2);
                 }
             }
-        }
+            // the next sub-chunk's hash (the next batch's keys, at a batch's end), then this
+            // flush's stores
+            if constexpr (u + 1 < P) {
+                hash_sub(s0 + kps, cw[F16 ? u + 1 : 0]);
+            } else {
+                if constexpr (F16) {
+#pragma unroll
+                    for (int x = 0; x < P; ++x) cw[x] = kw[x];
+                }
+                hash_sub(c0 + uint64_t(P) * kps, cw[0]);
+            }
+            put_groups(pd);
+            ++j;
+        };
+        static_assert(P == 2, "two sub-chunks per batch");
+        sub(std::integral_constant<int, 0>{});
+        sub(std::integral_constant<int, 1>{});
     }
     lds_barrier();
-    // The last partial group of every tile leaves as a whole group too (entries past the fill
-    // count are never read; the region has room: head is a multiple of GS and cap of 32).
     {
-        uint32_t* wd = desc + wave * kRingDescPerWave;
-        constexpr uint32_t lpg = GS / 4, gpi = 64 / lpg;
-        for (uint32_t b0 = wave * 64; b0 < B; b0 += nt) {
-            const uint32_t b = b0 + lane;
-            uint32_t hh = 0, tt = 0;
-            if (b < B) {
-                const uint32_t v = ht[b];
-                hh = v >> 16;
-                tt = v & 0xFFFFu;
-            }
-            const bool part = tt > hh;
-            const uint64_t m1 = __ballot(part);
-            const uint32_t at = __popcll(m1 & ((uint64_t(1) << lane) - 1)), total = __popcll(m1);
-            if (part) wd[at] = b | (hh << 12);
-            __builtin_amdgcn_wave_barrier();
-            for (uint32_t c = 0; c < total; c += gpi) {
-                const uint32_t gi = c + lane / lpg, q = lane % lpg;
-                if (gi < total) {
-                    const uint32_t d = wd[gi];
-                    const uint32_t tb = d & 0xFFFu;
-                    const uint32_t e = (d >> 12) + q * 4;
-                    const uint4 v = ring_group4(ring + tb * RC, e + ring_stagger(tb), rmask);
-                    st_stream<PROBE ? kNtProbePart : kNtBuildPart>(region_at(tb, e), v);
-                }
-            }
-            __builtin_amdgcn_wave_barrier();
-        }
+        // the last partial group leaves as a whole group too (entries past the fill count are
+        // never read; the region has room: head is a multiple of GS and cap of 32)
+        const uint32_t t4 = owner ? ht[tid] & 0xFFFFu : 0u;
+        write_groups(t4 > h4, h4);
     }
-    // fill counts; the probe's remaining cumulative counts
-    for (uint32_t b = tid; b < B; b += nt) {
-        const uint32_t t = ht[b] & 0xFFFFu;
-        fill[uint64_t(b) * pg.G + g] = t;
+    if (PBF_DIAG_SINK && (diag_x.x ^ diag_x.y ^ diag_x.z ^ diag_x.w) == 0x12345678u) fill[0] = 0;
+    if (owner) {
+        const uint32_t t4 = ht[tid] & 0xFFFFu;
+        // fill counts; the probe's remaining cumulative counts
+        fill[uint64_t(tid) * pg.G + g] = t4 >> 2;
         if constexpr (PROBE)
-            for (uint32_t q = (j + 3) >> 2; q <= pg.nq; ++q) pref[(uint64_t(g) * nqs + q) * B + b] = uint16_t(t);
+            for (uint32_t q = (j + 3) >> 2; q <= pg.nq; ++q) own_pref[uint64_t(q) * B] = uint16_t(t4 >> 2);
     }
     // the buffered spills (every append is done: the barrier above)
     const uint32_t ns = min(*nspill, pg.spill_cap);
     if (ns) {
         if constexpr (PROBE) {
-            for (uint32_t x = tid; x < ns; x += nt) spill_probe(ps, pos_to_bit(sbuf[2 * x], tm), k0 + sbuf[2 * x + 1]);
+            for (uint32_t x = tid; x < ns; x += blockDim.x) spill_probe(ps, pos_to_bit(sbuf[2 * x], tm), k0 + sbuf[2 * x + 1]);
         } else {
             lds_barrier();  // every thread has read nspill before the dump word takes the base
             if (tid == 0) smem[dump] = atomicAdd(ovf_count, ns);
             lds_barrier();
             const uint32_t base = smem[dump];
-            for (uint32_t x = tid; x < ns; x += nt) ovf[base + x] = sbuf[x];
+            for (uint32_t x = tid; x < ns; x += blockDim.x) ovf[base + x] = sbuf[x];
         }
     }
 }

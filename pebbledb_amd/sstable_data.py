@@ -99,6 +99,14 @@ def plan_blocks_native(ko: np.ndarray, vo: np.ndarray, block_size: int = BLOCK_S
     return bf[:nb.value + 1].copy(), bo[:nb.value + 1].copy()
 
 
+def _check_max_sstable_size(max_sstable_size: int) -> None:
+    """A split size of 0 or less is refused.  (The reference checks the position after every
+    add, lsm_storage.py:241, so there it would build one SSTable per record; the planners here
+    split where a block finishes, which agrees with it for every positive size.)"""
+    if max_sstable_size <= 0:
+        raise ValueError("max_sstable_size must be positive")
+
+
 def plan_compaction(ko: np.ndarray, vo: np.ndarray, block_size: int = BLOCK_SIZE,
                     max_sstable_size: int = 262_144_000):
     """Compaction's output split (``LsmStorage._compact``, src/lsm_storage.py:233-251) over a
@@ -116,6 +124,7 @@ def plan_compaction(ko: np.ndarray, vo: np.ndarray, block_size: int = BLOCK_SIZE
     n = len(ko) - 1
     if not 0 < block_size <= 65_536:
         raise ValueError("block_size must be in (0, 65536]: DataBlock offsets are u16 (blocks.py:34)")
+    _check_max_sstable_size(max_sstable_size)
     if n <= 0:
         return (np.zeros(1, np.uint64), np.zeros(1, np.uint64), np.zeros(1, np.uint64), 0)
     sizes = (np.diff(ko.astype(np.int64)) + np.diff(vo.astype(np.int64)) + RECORD_HEADER)
@@ -163,6 +172,7 @@ def plan_compaction_native(ko: np.ndarray, vo: np.ndarray, block_size: int = BLO
     n = len(ko) - 1
     if not 0 < block_size <= 65_536:
         raise ValueError("block_size must be in (0, 65536]: DataBlock offsets are u16 (blocks.py:34)")
+    _check_max_sstable_size(max_sstable_size)
     if n <= 0:
         return (np.zeros(1, np.uint64), np.zeros(1, np.uint64), np.zeros(1, np.uint64), 0)
     ko = np.ascontiguousarray(ko, dtype=np.uint64)

@@ -102,3 +102,17 @@ def test_native_planner_random_runs():
         for x, y in zip(a[:3], b[:3]):
             assert np.array_equal(x, y), trial
         assert a[3] == b[3], trial
+
+
+def test_non_positive_split_size_is_refused():
+    """max_sstable_size <= 0: the reference (position tested after every add, lsm_storage.py:241)
+    would build one SSTable per record; both planners refuse the size instead of silently
+    splitting at the first finished block (round-4 advice)."""
+    from pebbledb_amd.sstable_data import plan_compaction_native
+    ko = np.array([0, 3, 6], np.uint64)
+    vo = np.array([0, 10, 20], np.uint64)
+    for mx in (0, -1):
+        with pytest.raises(ValueError, match="max_sstable_size"):
+            plan_compaction(ko, vo, 1024, mx)
+        with pytest.raises(ValueError, match="max_sstable_size"):
+            plan_compaction_native(ko, vo, 1024, mx)

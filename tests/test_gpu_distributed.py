@@ -81,3 +81,63 @@ def test_two_ranks_one_gpu_hip_filters_equal_oracle(oracle):
         want = oracle.build(2 ** 18, 6, PackedKeys.fixed(splitmix_hex_keys(77, a, b - a)))
         assert np.array_equal(masks[f], oracle.probe(want, 6, probe)), f
         assert mat[f, a:b].all()
+
+
+_KEYS_WORKER = textwrap.dedent("""
+    import importlib.util, json, os, sys
+    sys.path.insert(0, '.')
+    import numpy as np
+    import torch.distributed as dist
+    from pebbledb_amd import BloomFilter, PackedKeys, may_contain_multi
+    from pebbledb_amd.keys import splitmix_hex_keys
+    from pebbledb_amd.shard import key_range
+    spec = importlib.util.spec_from_file_location("bench_mod", "bench.py")
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    dist.init_process_group("gloo", init_method="env://")
+    n_filters, kpf, nb, k, nq = 8, 40_000, 2 ** 18, 6, 8 * 40_000 + 5003
+    plan = bench.rank_plan("c5", world, rank, 0, c5_probes=nq)  # key-partitioned layout
+    a, b = plan["probe_keys"]
+    fs = []
+    for f in plan["filters"]:
+        lo, hi = key_range(f, kpf)
+        bf = BloomFilter(nb, k, device=0)
+        bf.add_many(PackedKeys.fixed(splitmix_hex_keys(77, lo, hi - lo)))
+        fs.append(bf)
+    probe = PackedKeys.fixed(splitmix_hex_keys(77, a, b - a))  # only this rank's slice
+    masks = may_contain_multi(fs, probe)
+    objs = [None] * world
+    dist.all_gather_object(objs, {"a": a, "b": b, "masks": [m.tobytes().hex() for m in masks]})
+    dist.barrier()
+    if rank == 0:
+        print("RESULT " + json.dumps(objs), flush=True)
+    dist.destroy_process_group()
+""")
+
+
+def test_two_ranks_key_partitioned_probe_equals_oracle(oracle):
+    """C5's key-partitioned layout (bench.rank_plan 'keys'): every rank holds the 8 filters and
+    probes its slice of the batch through the fused multi-filter path; the slices' masks,
+    concatenated, equal the oracle's whole-batch masks for every filter."""
+    from pebbledb_amd.keys import PackedKeys, splitmix_hex_keys
+    from pebbledb_amd.shard import key_range
+    world, port = 2, _free_port()
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, "-c", _KEYS_WORKER], env=env, cwd=REPO, stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True))
+    outs = [p.communicate(timeout=300) for p in procs]
+    for p, (o, e) in zip(procs, outs):
+        assert p.returncode == 0, e[-2000:]
+    parts = json.loads([x for x in outs[0][0].splitlines() if x.startswith("RESULT ")][0][7:])
+    nq = 8 * 40_000 + 5003
+    assert parts[0]["a"] == 0 and parts[-1]["b"] == nq and parts[0]["b"] == parts[1]["a"] and parts[0]["b"] % 64 == 0
+    probe = PackedKeys.fixed(splitmix_hex_keys(77, 0, nq))
+    for f in range(8):
+        got = np.concatenate([np.frombuffer(bytes.fromhex(p["masks"][f]), np.uint8) for p in parts])
+        lo, hi = key_range(f, 40_000)
+        want = oracle.probe(oracle.build(2 ** 18, 6, PackedKeys.fixed(splitmix_hex_keys(77, lo, hi - lo))), 6, probe)
+        assert np.array_equal(got, want), f

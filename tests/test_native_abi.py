@@ -72,3 +72,30 @@ def test_build_deps_cover_every_included_header():
     for f in os.listdir(csrc):
         if f.endswith(".hpp"):
             assert os.path.join(csrc, f) in deps, f
+
+
+def test_placement_groups_of_a_multi_device_probe_without_gpu():
+    """pbf_plan_groups is the placement step of pbf_probe_multi_placed (and of a host-batch
+    pbf_probe_multi over filters on several devices, grouped by device): the 8-GPU shape — 16
+    SSTable filters spread over devices 0..7 — gives 8 groups in first-appearance order, each
+    host thread's group on its own device; a group naming two devices is refused."""
+    import numpy as np
+    L = _native.lib()
+
+    def plan(groups, devices):
+        g = np.ascontiguousarray(groups, dtype=np.uint32)
+        d = np.ascontiguousarray(devices, dtype=np.int32)
+        slot = np.zeros(len(g), dtype=np.uint32)
+        ng = ctypes.c_uint32(0)
+        rc = L.pbf_plan_groups(g.ctypes.data, d.ctypes.data, len(g), slot.ctypes.data, ctypes.byref(ng))
+        return rc, slot.tolist(), ng.value
+
+    devices = [f % 8 for f in range(16)][::-1]  # filters on devices 7..0, 7..0
+    rc, slot, ng = plan(devices, devices)  # by device, as pbf_probe_multi groups them
+    assert rc == 0 and ng == 8
+    assert slot == [0, 1, 2, 3, 4, 5, 6, 7] * 2  # device 7 first (first appearance), then 6, ...
+    rc, slot, ng = plan([5, 5, 9, 5], [2, 2, 2, 2])  # two groups on one device are allowed
+    assert rc == 0 and ng == 2 and slot == [0, 0, 1, 0]
+    rc, _, _ = plan([1, 1], [0, 3])
+    assert rc == _native.PBF_ERR_INVALID and b"share a device" in L.pbf_last_error()
+    assert plan([], []) [0] == 0

@@ -82,6 +82,12 @@ for step in "$@"; do
     prof_c4) prof prof_c4 600 --config c4 --steps 2 --warmup 1 --no-cpu-baseline ;;
     prof_c5) prof prof_c5 600 --config c5 --steps 3 --warmup 1 --no-cpu-baseline --no-host-c5 ;;
     ab) ab ab 300 2 --steps 50 --warmup 5 ;;
+    ab1) ab ab 300 1 --steps 50 --warmup 5 ;;
+    profab) prof profq_default 300 --steps 20 --warmup 5 --no-cpu-baseline --no-host-inclusive
+            for v in build/variants/*.so; do
+              nm=$(basename $v .so)
+              PBF_LIB=$PWD/$v prof profq_$nm 300 --steps 20 --warmup 5 --no-cpu-baseline --no-host-inclusive
+            done ;;
     unaligned) run unaligned 120 tools/microbench/unaligned_loads ;;
     parity_var) for v in build/variants/*.so; do
                   nm=$(basename $v .so)
