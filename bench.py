@@ -292,6 +292,20 @@ def dropin_latency(device, reps=2000):
                      "hits": hits, "bitmap_sha16": __import__("hashlib").sha256(blob).hexdigest()[:16]}
         if cls is BloomFilter:
             out[name]["build_from_keys_1k_us"] = round(t_bk / 20 * 1e6, 1)
+            # where the per-key time goes: the same calls with a launch per key (the resident
+            # reader off)
+            L = _native_lib()
+            L.pbf_resident_enable(0)
+            try:
+                for k in probes[:50]:
+                    bf.may_contain(k)
+                t0 = time.perf_counter()
+                hits_l = sum(bf.may_contain(probes[i % 1000]) for i in range(reps))
+                out[name]["may_contain_launch_us"] = round((time.perf_counter() - t0) / reps * 1e6, 2)
+                out[name]["launch_hits_equal"] = hits_l == hits
+            finally:
+                L.pbf_resident_enable(1)
+
     out["identical"] = (out["pebbledb_amd"]["bitmap_sha16"] == out["reference_port"]["bitmap_sha16"]
                         and out["pebbledb_amd"]["hits"] == out["reference_port"]["hits"])
     out["get_16_filters"] = get_set_latency(device)
@@ -299,11 +313,16 @@ def dropin_latency(device, reps=2000):
     return out
 
 
+def _native_lib():
+    from pebbledb_amd import _native
+    return _native.lib()
+
+
 def get_set_latency(device, reps=1000):
     """One LsmStorage.get's bloom checks (src/lsm_storage.py:164-179) over 10 L0 + 6 level SSTable
     filters of 16 different sizes (product sizing, sstable.py:274: 20k..170k keys, k = 10): one
-    pbf_may_contain_set launch (lsm_get.candidates_one) vs 16 may_contain calls (one launch each);
-    the answers must be identical."""
+    pbf_may_contain_set call (lsm_get.candidates_one; answered by the resident reader, and with it
+    off by one k_may_contain_set launch) vs 16 may_contain calls; the answers must be identical."""
     from pebbledb_amd import BloomFilter
     from pebbledb_amd.keys import splitmix_hex_keys_str
     from pebbledb_amd.lsm_get import LevelTable, candidates_one
@@ -325,9 +344,21 @@ def get_set_latency(device, reps=1000):
     t0 = time.perf_counter()
     loop = [[t for t, bf in enumerate(flat) if bf.may_contain(probes[i % 1000])] for i in range(reps)]
     t_loop = time.perf_counter() - t0
+    L = _native_lib()
+    L.pbf_resident_enable(0)  # the same gets with one k_may_contain_set launch each
+    try:
+        for key in probes[:50]:
+            candidates_one(key, l0, levels)
+        t0 = time.perf_counter()
+        launched = [candidates_one(probes[i % 1000], l0, levels) for i in range(reps)]
+        t_launch = time.perf_counter() - t0
+    finally:
+        L.pbf_resident_enable(1)
     return {"filters": len(flat), "nb_bytes": [bf.nb_bytes for bf in flat],
-            "one_launch_us_per_get": round(t_set / reps * 1e6, 2),
-            "may_contain_x16_us_per_get": round(t_loop / reps * 1e6, 2), "identical": one == loop}
+            "one_call_us_per_get": round(t_set / reps * 1e6, 2),
+            "one_launch_us_per_get": round(t_launch / reps * 1e6, 2),
+            "may_contain_x16_us_per_get": round(t_loop / reps * 1e6, 2),
+            "identical": one == loop == launched}
 
 
 def reader_threads(device, calls=4000):

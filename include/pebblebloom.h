@@ -60,6 +60,8 @@ extern "C" {
 #define PBF_DETAIL_ONE_KEY 4 /* pbf_may_contain's one-key launch */
 #define PBF_DETAIL_SET 8     /* multi-filter direct probe (k_probe_set: each key hashed once for the set) */
 #define PBF_DETAIL_PACKED 16 /* tiled build: region entries packed three positions per 8 bytes */
+#define PBF_DETAIL_SHARED 32 /* one-key probe under the handle's lock held shared (a reader stream) */
+#define PBF_DETAIL_RESIDENT 64 /* one-key probe answered by the resident reader wave (no launch per key) */
 
 typedef struct pbf_filter pbf_filter_t;
 
@@ -148,6 +150,18 @@ int pbf_may_contain(pbf_filter_t* f, const uint8_t* key, uint64_t len, int* out)
  * mapped pinned memory; synchronous.  All filters on one device (a filter may repeat). */
 int pbf_may_contain_set(pbf_filter_t* const* filters, uint32_t nfilters, const uint8_t* key, uint64_t len,
                         uint8_t* out_bits);
+
+/* pbf_may_contain / pbf_may_contain_set on built, idle filters (nothing queued on their streams)
+ * are answered by a resident reader: ONE wave per device stays on a stream of its own while keys
+ * arrive, polling per-thread request slots in mapped pinned memory (no launch per key); it leaves
+ * after PBF_RESIDENT_IDLE_US (default 2000) without a key and is relaunched by the next one.
+ * PBF_RESIDENT_READER=0 (read once) launches per key instead.  Keys over 1024 bytes, k > 32 and
+ * threads beyond 64 per device take the per-key launch.  *launches = the waves started so far on
+ * `device` (0 before the first resident answer). */
+int pbf_resident_launches(int device, uint32_t* launches);
+/* Turns the resident reader on (1) or off (0) for later calls of the process (overrides
+ * PBF_RESIDENT_READER; a wave already resident leaves after its idle time). */
+int pbf_resident_enable(int on);
 
 /* mmh3.hash(key, seed) (bloom_filter.py:46: MurmurHash3_x86_32, signed int32) of one host key
  * of at most 4096 bytes, computed on `device` (one launch). */

@@ -20,6 +20,8 @@ PBF_ERR_ZERO_SIZE = -3
 PBF_BUILD_AUTO, PBF_BUILD_ATOMIC, PBF_BUILD_TILED = 0, 1, 2
 PBF_PROBE_AUTO, PBF_PROBE_DIRECT, PBF_PROBE_TILED = 0, 1, 2
 PBF_DETAIL_RING, PBF_DETAIL_SORT, PBF_DETAIL_ONE_KEY, PBF_DETAIL_SET, PBF_DETAIL_PACKED = 1, 2, 4, 8, 16
+PBF_DETAIL_SHARED = 32
+PBF_DETAIL_RESIDENT = 64
 
 _u8p = ctypes.c_void_p
 _vp = ctypes.c_void_p
@@ -38,6 +40,8 @@ SIGNATURES = {
     "pbf_add": (_int, [_vp, _u8p, _vp, _u64, _int]),
     "pbf_build": (_int, [_vp, _u8p, _vp, _u64, _int]),
     "pbf_murmur3_x86_32": (_int, [_int, ctypes.c_char_p, _u64, _u32, ctypes.POINTER(ctypes.c_int32)]),
+    "pbf_resident_launches": (_int, [_int, ctypes.POINTER(_u32)]),
+    "pbf_resident_enable": (_int, [_int]),
     "pbf_probe_fixed": (_int, [_vp, _u8p, _u32, _u64, _u8p, _int]),
     "pbf_probe": (_int, [_vp, _u8p, _vp, _u64, _u8p, _int]),
     "pbf_probe_multi_fixed": (_int, [_vp, _u32, _u8p, _u32, _u64, _vp, _int]),

@@ -32,6 +32,7 @@
 #include "sstable_kernels.hpp"
 #include "lsm_kernels.hpp"
 #include "set_kernels.hpp"
+#include "reader_service.hpp"
 
 using namespace pbf;
 
@@ -913,7 +914,14 @@ int run_tiled_probe_set(pbf_filter_t* f, pbf_filter_t* const* fs, uint32_t nf, c
     const uint32_t S = pl.gsplit;
     const bool use_hw = S > 1 || nf > 1;
     uint32_t* hw = nullptr;
-    if (use_hw) {
+    // one filter, whole 32-key words, a 4-byte aligned mask: the gather's ANDed words ARE the
+    // LSB-first hit mask (bit i of word w = key 32w + i, little-endian), so it ANDs into the
+    // caller's mask directly and no conversion kernel runs
+    const bool hw_is_mask = use_hw && nf == 1 && b.n % 32 == 0 &&
+                            (reinterpret_cast<uintptr_t>(hitmasks[0] + hm_off) & 3) == 0;
+    if (hw_is_mask) {
+        hw = reinterpret_cast<uint32_t*>(hitmasks[0] + hm_off);
+    } else if (use_hw) {
         HIP_TRY(sc->hw.ensure(neg_bytes * nf));
         hw = static_cast<uint32_t*>(sc->hw.p);
     }
@@ -978,7 +986,7 @@ int run_tiled_probe_set(pbf_filter_t* f, pbf_filter_t* const* fs, uint32_t nf, c
     gather<<<grid, gthreads, pl.lds_gather, s>>>(tm, pg, b.n, regions, R, fill, pref, neg, hitmasks[0] + hm_off, hw, nf,
                                            r_words, neg_words, pl.gtq);
     LAUNCHED(f, "k_gather_ring");
-    if (use_hw) {  // every filter's hit mask in one launch
+    if (use_hw && !hw_is_mask) {  // every filter's hit mask in one launch
         HitMasks hms{};
         for (uint32_t i = 0; i < nf; ++i) hms.hm[i] = hitmasks[i] + hm_off;
         const dim3 hgrid(std::max<uint32_t>(1, grid_for(neg_words, 256, 4096) / nf), nf);
@@ -1703,6 +1711,212 @@ hipError_t reader_stream(int device, hipStream_t* out) {
     return hipSuccess;
 }
 
+// ---------------------------------------------------------------- resident one-key reader
+// (reader_service.hpp) One board per device in mapped, coherent pinned memory, one resident
+// wave serving it on a stream with a CU mask (a stream with a CU mask gets a hardware queue of
+// its own, so the resident wave never holds up other streams' work), one slot per host thread.
+// PBF_RESIDENT_READER=0 sends every one-key probe through the per-key launch instead;
+// PBF_RESIDENT_IDLE_US (default 2000) is how long the wave waits for a key before it leaves.
+struct ResidentReader {
+    std::mutex mu;
+    SvcBoard* host = nullptr;
+    SvcBoard* dev = nullptr;
+    hipStream_t stream = nullptr;
+    hipEvent_t done = nullptr;  // recorded after each launch: the wave has left once it completes
+    bool launched = false;
+    uint32_t launches = 0;
+    uint32_t nslots = 0;
+    std::vector<uint32_t> free_slots;
+    uint64_t idle_ticks = 0, life_ticks = 0;
+    int device = 0;
+};
+
+std::atomic<int> g_resident_on{-1};  // -1: PBF_RESIDENT_READER not read yet
+
+bool resident_enabled() {
+    int on = g_resident_on.load(std::memory_order_relaxed);
+    if (on < 0) {
+        const char* e = std::getenv("PBF_RESIDENT_READER");
+        int want = (e && e[0] == '0') ? 0 : 1;
+        int expected = -1;
+        g_resident_on.compare_exchange_strong(expected, want);
+        on = g_resident_on.load(std::memory_order_relaxed);
+    }
+    return on != 0;
+}
+
+std::mutex g_resident_mu;
+std::map<int, ResidentReader*> g_resident;  // never freed: a wave may still poll its board at exit
+
+// At exit: every resident wave is told to leave and given a few milliseconds to do so (it
+// leaves by itself after its idle time anyway).
+void resident_shutdown() {
+    std::lock_guard<std::mutex> lock(g_resident_mu);
+    for (auto& kv : g_resident) {
+        ResidentReader* rr = kv.second;
+        if (!rr || !rr->host) continue;
+        __atomic_store_n(&rr->host->stop, 1u, __ATOMIC_RELEASE);
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    for (auto& kv : g_resident) {
+        ResidentReader* rr = kv.second;
+        if (!rr || !rr->host) continue;
+        while (__atomic_load_n(&rr->host->state, __ATOMIC_ACQUIRE) != 0 &&
+               std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(20)) {
+        }
+    }
+}
+
+// The device's reader (created on first use), or nullptr if it cannot be set up (the caller
+// then launches per key).
+ResidentReader* resident_reader(int device) {
+    std::lock_guard<std::mutex> lock(g_resident_mu);
+    auto it = g_resident.find(device);
+    if (it != g_resident.end()) return it->second;
+    ResidentReader* rr = nullptr;
+    do {
+        void* h = nullptr;
+        if (hipHostMalloc(&h, sizeof(SvcBoard), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) break;
+        std::memset(h, 0, sizeof(SvcBoard));
+        void* d = nullptr;
+        if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
+            (void)hipHostFree(h);
+            break;
+        }
+        int ncu = 0, khz = 0;
+        if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
+            hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) != hipSuccess || ncu <= 0 || khz <= 0) {
+            (void)hipHostFree(h);
+            break;
+        }
+        std::vector<uint32_t> mask((size_t(ncu) + 31) / 32, ~0u);
+        if (ncu % 32) mask.back() = (1u << (ncu % 32)) - 1u;
+        hipStream_t st = nullptr;
+        if (hipExtStreamCreateWithCUMask(&st, uint32_t(mask.size()), mask.data()) != hipSuccess) {
+            (void)hipHostFree(h);
+            break;
+        }
+        hipEvent_t ev = nullptr;
+        if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+            (void)hipStreamDestroy(st);
+            (void)hipHostFree(h);
+            break;
+        }
+        rr = new ResidentReader();
+        rr->host = static_cast<SvcBoard*>(h);
+        rr->dev = static_cast<SvcBoard*>(d);
+        rr->stream = st;
+        rr->done = ev;
+        rr->device = device;
+        const char* e = std::getenv("PBF_RESIDENT_IDLE_US");
+        const uint64_t idle_us = e && std::atoi(e) > 0 ? uint64_t(std::atoi(e)) : 2000;
+        rr->idle_ticks = uint64_t(khz) * idle_us / 1000;
+        rr->life_ticks = uint64_t(khz) * 200;  // 200 ms
+        if (g_resident.empty()) std::atexit(resident_shutdown);
+    } while (false);
+    (void)hipGetLastError();
+    g_resident[device] = rr;
+    return rr;
+}
+
+// A wave serving rr's board: launch one unless the last launch is still running (or queued).
+int resident_ensure(ResidentReader* rr) {
+    std::lock_guard<std::mutex> lock(rr->mu);
+    if (rr->launched) {
+        const hipError_t q = hipEventQuery(rr->done);
+        if (q == hipErrorNotReady) {
+            (void)hipGetLastError();
+            return PBF_OK;
+        }
+        HIP_TRY(q);
+    }
+    HIP_TRY(hipSetDevice(rr->device));
+    k_reader_service<<<1, 64, 0, rr->stream>>>(rr->dev, ++rr->launches, rr->idle_ticks, rr->life_ticks);
+    CHECK_LAUNCH();
+    HIP_TRY(hipEventRecord(rr->done, rr->stream));
+    rr->launched = true;
+    return PBF_OK;
+}
+
+// The calling thread's slot on a device's board (returned to the board when the thread ends).
+struct ResidentSlot {
+    ResidentReader* rr = nullptr;
+    int slot = -1;
+    uint32_t seq = 0;
+    ResidentSlot() = default;
+    ResidentSlot(const ResidentSlot&) = delete;
+    ResidentSlot& operator=(const ResidentSlot&) = delete;
+    ~ResidentSlot() {
+        if (rr && slot >= 0) {
+            std::lock_guard<std::mutex> lock(rr->mu);
+            rr->free_slots.push_back(uint32_t(slot));
+        }
+    }
+};
+
+// One key against nf filters sharing k through the resident reader: *bits (bit f = filters f's
+// answer) and *taken = true, or *taken = false when this call cannot use it (disabled, key or
+// set too large, no free slot, no board): the caller launches per key.  The filters' bitmaps
+// must have no work still queued (reader_ok).
+int resident_probe(int device, const SvcFilter* fs, uint32_t nf, uint32_t k, const uint8_t* key, uint64_t len,
+                   uint64_t* bits, bool* taken) {
+    *taken = false;
+    if (!resident_enabled() || len > kSvcKeyMax || k == 0 || k > 32 || nf == 0 || nf > kSvcFilters) return PBF_OK;
+    thread_local std::map<int, ResidentSlot> mine;
+    ResidentSlot& ts = mine[device];
+    if (ts.slot < 0) {
+        ResidentReader* rr = resident_reader(device);
+        if (!rr) return PBF_OK;
+        std::lock_guard<std::mutex> lock(rr->mu);
+        uint32_t slot;
+        if (!rr->free_slots.empty()) {
+            slot = rr->free_slots.back();
+            rr->free_slots.pop_back();
+        } else if (rr->nslots < kSvcSlots) {
+            slot = rr->nslots++;
+            __atomic_store_n(&rr->host->nused, rr->nslots, __ATOMIC_RELEASE);
+        } else {
+            return PBF_OK;  // 64 threads hold slots: launch per key
+        }
+        ts.rr = rr;
+        ts.slot = int(slot);
+        ts.seq = __atomic_load_n(&rr->host->head[slot].req, __ATOMIC_ACQUIRE);  // a recycled slot's last
+    }
+    ResidentReader* rr = ts.rr;
+    SvcHead& hd = rr->host->head[ts.slot];
+    SvcSlot& sl = rr->host->slot[ts.slot];
+    std::memcpy(sl.f, fs, size_t(nf) * sizeof(SvcFilter));
+    if (len) std::memcpy(sl.key, key, len);
+    uint32_t seq = ts.seq + 1;
+    if (seq == 0) seq = 1;
+    ts.seq = seq;
+    hd.nf = nf;
+    hd.len = uint32_t(len);
+    hd.k = k;
+    __atomic_store_n(&hd.req, seq, __ATOMIC_RELEASE);  // the body and the head's fields before it
+    int rc = PBF_OK;
+    if (__atomic_load_n(&rr->host->state, __ATOMIC_ACQUIRE) == 0) {
+        rc = resident_ensure(rr);
+        if (rc) return rc;
+    }
+    // the answer: poll the slot's ack; a wave that left after its last look at the heads (the
+    // request stranded) is relaunched
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t spin = 1; __atomic_load_n(&sl.ack, __ATOMIC_ACQUIRE) != seq; ++spin) {
+        if ((spin & 63) == 0) {
+            const auto el = std::chrono::steady_clock::now() - t0;
+            if (el > std::chrono::microseconds(50) && __atomic_load_n(&rr->host->state, __ATOMIC_ACQUIRE) == 0) {
+                rc = resident_ensure(rr);
+                if (rc) return rc;
+            }
+            if (el > std::chrono::seconds(2)) return fail(PBF_ERR_HIP, "resident reader: no answer within 2 s");
+        }
+    }
+    *bits = __atomic_load_n(&sl.bits, __ATOMIC_ACQUIRE);
+    *taken = true;
+    return PBF_OK;
+}
+
 // Whether a one-key probe of f may run under f's lock held SHARED: the filter is materialised,
 // nothing of it is still queued on its stream (its last build / from_bytes has completed, so a
 // reader stream sees the finished bitmap), and the key takes the mapped one-key kernel.
@@ -1725,6 +1939,19 @@ bool reader_ok(pbf_filter_t* f, uint64_t len) {
 // held), so nothing of the handle is written but the probe diagnostics (atomics).
 int one_key_probe(pbf_filter_t* f, const uint8_t* key, uint64_t len, int* out, hipStream_t s, bool shared) {
     int rc = PBF_OK;
+    if (shared) {  // no work of f queued (reader_ok): the resident reader may answer
+        SvcFilter sf{f->bitmap, f->im};
+        uint64_t bits = 0;
+        bool taken = false;
+        rc = resident_probe(f->device, &sf, 1, f->k, key, len, &bits, &taken);
+        if (rc) return rc;
+        if (taken) {
+            *out = int(bits & 1u);
+            f->last_probe_mode = PBF_PROBE_DIRECT;
+            f->last_probe_detail = PBF_DETAIL_ONE_KEY | PBF_DETAIL_SHARED | PBF_DETAIL_RESIDENT;
+            return PBF_OK;
+        }
+    }
     OneKeyStage* st = nullptr;
     rc = one_key_stage(f->device, &st);
     if (rc) return rc;
@@ -1771,7 +1998,7 @@ int one_key_probe(pbf_filter_t* f, const uint8_t* key, uint64_t len, int* out, h
     if (hit > 1) return fail(PBF_ERR_HIP, "one-key probe: result byte not written");
     *out = hit;
     f->last_probe_mode = PBF_PROBE_DIRECT;
-    f->last_probe_detail = PBF_DETAIL_ONE_KEY;
+    f->last_probe_detail = PBF_DETAIL_ONE_KEY | (shared ? PBF_DETAIL_SHARED : 0u);
     return PBF_OK;
 }
 
@@ -1858,13 +2085,30 @@ int may_contain_set_locked(pbf_filter_t* const* fs, uint32_t nf, const uint8_t* 
     if (rc) return rc;
     if (len) std::memcpy(st->host + kOneKeyData, key, len);
     hipStream_t s = shared ? rs : f0->stream;
+    std::vector<uint8_t> resident_set(nf, 0);  // filters the resident reader answered
     for (uint32_t k : ks) {
         std::vector<uint32_t> idx;
         for (uint32_t i = 0; i < nf; ++i)
             if (fs[i]->k == k) idx.push_back(i);
         for (size_t c0 = 0; c0 < idx.size(); c0 += kMaxFilterSet) {
+            const uint32_t nsub = uint32_t(std::min<size_t>(kMaxFilterSet, idx.size() - c0));
+            if (shared) {  // every handle reader_ok: the resident reader may answer
+                SvcFilter sf[kMaxFilterSet];
+                for (uint32_t j = 0; j < nsub; ++j) sf[j] = SvcFilter{fs[idx[c0 + j]]->bitmap, fs[idx[c0 + j]]->im};
+                uint64_t bits = 0;
+                bool taken = false;
+                rc = resident_probe(f0->device, sf, nsub, k, key, len, &bits, &taken);
+                if (rc) return rc;
+                if (taken) {
+                    for (uint32_t j = 0; j < nsub; ++j) {
+                        put(idx[c0 + j], (bits >> j) & 1u);
+                        resident_set[idx[c0 + j]] = 1;
+                    }
+                    continue;
+                }
+            }
             FilterSet fset{};
-            fset.nf = uint32_t(std::min<size_t>(kMaxFilterSet, idx.size() - c0));
+            fset.nf = nsub;
             for (uint32_t j = 0; j < fset.nf; ++j) {
                 pbf_filter_t* f = fs[idx[c0 + j]];
                 if (!shared) {
@@ -1912,7 +2156,7 @@ int may_contain_set_locked(pbf_filter_t* const* fs, uint32_t nf, const uint8_t* 
     for (uint32_t i = 0; i < nf; ++i) {
         if (std::find(ks.begin(), ks.end(), fs[i]->k) == ks.end()) continue;
         fs[i]->last_probe_mode = PBF_PROBE_DIRECT;
-        fs[i]->last_probe_detail = PBF_DETAIL_ONE_KEY | PBF_DETAIL_SET;
+        fs[i]->last_probe_detail = PBF_DETAIL_ONE_KEY | PBF_DETAIL_SET | (resident_set[i] ? PBF_DETAIL_RESIDENT : 0u);
     }
     return PBF_OK;
 }
@@ -2278,6 +2522,27 @@ int pbf_signal_stream(pbf_filter_t* f, void* stream) {
     if (!f->sig_ev) HIP_TRY(hipEventCreateWithFlags(&f->sig_ev, hipEventDisableTiming));
     HIP_TRY(hipEventRecord(f->sig_ev, f->stream));
     HIP_TRY(hipStreamWaitEvent(s, f->sig_ev, 0));
+    return PBF_OK;
+}
+
+int pbf_resident_enable(int on) {
+    g_resident_on.store(on ? 1 : 0);
+    return PBF_OK;
+}
+
+int pbf_resident_launches(int device, uint32_t* launches) {
+    if (!launches) return fail(PBF_ERR_INVALID, "null out");
+    *launches = 0;
+    ResidentReader* rr = nullptr;
+    {
+        std::lock_guard<std::mutex> lock(g_resident_mu);
+        auto it = g_resident.find(device);
+        if (it != g_resident.end()) rr = it->second;
+    }
+    if (rr) {
+        std::lock_guard<std::mutex> lock(rr->mu);
+        *launches = rr->launches;
+    }
     return PBF_OK;
 }
 

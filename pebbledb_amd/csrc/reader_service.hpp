@@ -1,0 +1,186 @@
+// Resident one-key reader for the per-key calls of LsmStorage.get (reference src/lsm_storage.py:
+// 164-179: `sstable.bloom_filter.may_contain(key)` = bloom_filter.py:67-74, per filter), gfx950.
+//
+// A launch per key costs the host's launch path and the GPU's dispatch on every call (~9 us of
+// the ~12 us a may_contain took).  Instead ONE wave stays resident on a stream of its own while
+// keys arrive: host threads post requests into slots of a board in mapped, coherent pinned host
+// memory and the wave polls the slots' 16-byte heads over the bus (lane s reads slot s), answers
+// every posted request and writes the answer and the request's sequence number back.  The wave
+// leaves after `idle` ticks without a request (and after `life` ticks whatever happens, so it
+// never holds its queue for long), and on the board's stop word; the host relaunches it when a
+// request finds it gone (pebblebloom.hip: ResidentReader).
+//
+// Per request (one key against up to 64 filters sharing k, like k_may_contain_set): the key is
+// copied into LDS (one 16-B load per lane), lane s hashes seed s (MurmurHash3_x86_32, seeds
+// 0..k-1), lane f gathers the k hashes from the other lanes and tests filter f's k bits, one
+// ballot is the answer.  Every load of host memory is volatile (the board changes under the
+// kernel: no load may be hoisted out of the poll loop or served from a cache), and the bitmap
+// words are read with device-scope atomic loads, so a filter rebuilt on another XCD since the
+// wave started is never read from a stale line of this XCD's L2 (the host only posts keys for a
+// filter with no work still queued on its stream).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "murmur_device.hpp"
+
+namespace pbf {
+
+constexpr uint32_t kSvcSlots = 64;     // host threads with a slot (one lane each)
+constexpr uint32_t kSvcKeyMax = 1024;  // longer keys take the launch path
+constexpr uint32_t kSvcFilters = 64;   // filters per request (one lane each)
+
+struct SvcFilter {  // 32 B
+    const uint32_t* bm;
+    IndexMap im;
+};
+static_assert(sizeof(SvcFilter) == 32, "SvcFilter layout");
+
+// Slot s's request head (host-written, `req` last): one lane's poll reads it whole.
+struct SvcHead {
+    uint32_t req;  // sequence number of the posted request (never 0)
+    uint32_t nf;   // filters (1..kSvcFilters)
+    uint32_t len;  // key bytes (<= kSvcKeyMax)
+    uint32_t k;    // hash functions (1..32), shared by the request's filters
+};
+
+struct SvcSlot {
+    uint32_t ack;      // device: the sequence answered, stored after `bits`
+    uint32_t pad0;
+    uint64_t bits;     // device: bit f = filters[f] may contain the key
+    uint8_t pad1[48];  // the body starts on its own 64-B line
+    SvcFilter f[kSvcFilters];
+    alignas(16) uint8_t key[kSvcKeyMax];
+};
+
+struct SvcBoard {
+    uint32_t stop;    // host: nonzero, the wave leaves at its next poll
+    uint32_t nused;   // host: slots [0, nused) may hold requests (the lanes that poll)
+    uint32_t state;   // device: launch id while serving, 0 once the wave has left
+    uint32_t served;  // device: requests answered by the last launch
+    uint32_t pad[12];
+    SvcHead head[kSvcSlots];
+    SvcSlot slot[kSvcSlots];
+};
+
+__device__ __forceinline__ uint4 vload16(const void* p) {
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    const v4u x = *reinterpret_cast<const volatile v4u*>(p);
+    return make_uint4(x.x, x.y, x.z, x.w);
+}
+__device__ __forceinline__ uint32_t vload4(const void* p) { return *reinterpret_cast<const volatile uint32_t*>(p); }
+
+// Filter fd's k bits (lanes f < nf) for the hashes held by lanes 0..k-1 (k <= KMAX): every
+// lane takes part in the shuffles (a lane reading an inactive lane's register gets no data), then
+// the k loads of a filter go out together.
+template <int KMAX>
+__device__ __forceinline__ bool svc_test(uint32_t h, uint32_t k, bool active, const SvcFilter& fd) {
+    uint32_t hv[KMAX];
+#pragma unroll
+    for (int q = 0; q < KMAX; ++q) hv[q] = __shfl(h, q, 64);
+    if (!active) return false;
+    uint32_t w[KMAX], sh[KMAX];
+#pragma unroll
+    for (int q = 0; q < KMAX; ++q) {
+        const uint64_t idx = py_index(hv[q], fd.im);
+        sh[q] = uint32_t(idx & 31);
+        w[q] = uint32_t(q) < k ? __hip_atomic_load(fd.bm + (idx >> 5), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : ~0u;
+    }
+    uint32_t acc = 1u;
+#pragma unroll
+    for (int q = 0; q < KMAX; ++q) acc &= w[q] >> sh[q];
+    return (acc & 1u) != 0u;
+}
+
+// One request of slot s: the key from host memory into LDS, one seed per lane, filter f on lane f.
+__device__ __forceinline__ void svc_answer(SvcBoard* b, uint32_t s, uint32_t req, uint32_t nf, uint32_t len, uint32_t k,
+                                           uint32_t* kw) {
+    const uint32_t lane = threadIdx.x;
+    SvcSlot* sl = b->slot + s;
+    // the key: 16 B per lane (the slot's key buffer is 16-B aligned and kSvcKeyMax = 64 x 16)
+    if (lane * 16 < len) {
+        const uint4 w = vload16(sl->key + lane * 16);
+        kw[lane * 4] = w.x;
+        kw[lane * 4 + 1] = w.y;
+        kw[lane * 4 + 2] = w.z;
+        kw[lane * 4 + 3] = w.w;
+    }
+    // filter f's descriptor (issued beside the key loads)
+    uint4 d0 = make_uint4(0, 0, 0, 0), d1 = d0;
+    if (lane < nf) {
+        d0 = vload16(&sl->f[lane]);
+        d1 = vload16(reinterpret_cast<const uint8_t*>(&sl->f[lane]) + 16);
+    }
+    __syncthreads();
+    // lane s: MurmurHash3_x86_32(key, seed s) (bloom_filter.py:46, mmh3.hash(key, s))
+    uint32_t h = lane;
+    const uint32_t nb = len >> 2, t = len & 3;
+    for (uint32_t i = 0; i < nb; ++i) h = round_h(h, mix_block(kw[i]));
+    if (t) h ^= mix_block(kw[nb] & ((1u << (8 * t)) - 1u));
+    h = fmix32(h ^ len);
+    SvcFilter fd;
+    fd.bm = reinterpret_cast<const uint32_t*>(uint64_t(d0.x) | (uint64_t(d0.y) << 32));
+    fd.im.m = uint64_t(d0.z) | (uint64_t(d0.w) << 32);
+    fd.im.magic = uint64_t(d1.x) | (uint64_t(d1.y) << 32);
+    fd.im.mode = d1.z;
+    fd.im.mask = d1.w;
+    // the AND of bloom_filter.py:71-74, without its early exit: the k loads go out together
+    const bool act = lane < nf;
+    const bool hit = k <= 4    ? svc_test<4>(h, k, act, fd)
+                     : k <= 8  ? svc_test<8>(h, k, act, fd)
+                     : k <= 16 ? svc_test<16>(h, k, act, fd)
+                               : svc_test<32>(h, k, act, fd);
+    const unsigned long long bal = __ballot(hit);
+    if (lane == 0) {
+        __hip_atomic_store(&sl->bits, uint64_t(bal), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&sl->ack, req, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    __syncthreads();  // kw is rewritten by the next request
+}
+
+// The resident wave (one workgroup of 64 threads).  `id` is the launch's id (state while it
+// serves); ticks are wall-clock ticks (hipDeviceAttributeWallClockRate).
+__global__ void __launch_bounds__(64) k_reader_service(SvcBoard* b, uint32_t id, uint64_t idle_ticks, uint64_t life_ticks) {
+    __shared__ uint32_t kw[kSvcKeyMax / 4 + 4];
+    const uint32_t lane = threadIdx.x;
+    uint32_t done = vload4(&b->slot[lane].ack);  // a relaunch resumes from the answered sequences
+    if (lane == 0) __hip_atomic_store(&b->state, id, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    const uint64_t t0 = wall_clock64();
+    uint64_t t_last = t0;
+    uint32_t served = 0;
+    while (true) {
+        const uint4 ctl = vload16(&b->stop);  // stop, nused
+        if (ctl.x) break;
+        const uint4 hd = lane < ctl.y ? vload16(&b->head[lane]) : make_uint4(done, 0, 0, 0);
+        const bool fresh = hd.x != done;
+        uint64_t pend = __ballot(fresh);
+        if (pend) {
+            while (pend) {
+                const uint32_t s = uint32_t(__builtin_ctzll(pend));
+                pend &= pend - 1;
+                const uint32_t req = __shfl(hd.x, int(s), 64), nf = __shfl(hd.y, int(s), 64);
+                const uint32_t len = __shfl(hd.z, int(s), 64), k = __shfl(hd.w, int(s), 64);
+                // a malformed head (the host never posts one) is acknowledged with no hits
+                if (nf >= 1 && nf <= kSvcFilters && len <= kSvcKeyMax && k >= 1 && k <= 32) {
+                    svc_answer(b, s, req, nf, len, k, kw);
+                } else if (lane == 0) {
+                    __hip_atomic_store(&b->slot[s].bits, uint64_t(0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    __hip_atomic_store(&b->slot[s].ack, req, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+                }
+                ++served;
+            }
+            if (fresh) done = hd.x;
+            t_last = wall_clock64();
+            continue;
+        }
+        const uint64_t now = wall_clock64();
+        if (now - t_last > idle_ticks || now - t0 > life_ticks) break;
+        __builtin_amdgcn_s_sleep(2);
+    }
+    if (lane == 0) {
+        __hip_atomic_store(&b->served, served, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&b->state, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+}  // namespace pbf

@@ -55,6 +55,21 @@ constexpr int kRingPrefetch = 2;
 #ifndef PBF_DIAG_WMASK
 #define PBF_DIAG_WMASK 0xFFFFFFFFu
 #endif
+#ifndef PBF_SPREAD_STORES
+#define PBF_SPREAD_STORES 0
+#endif
+#ifndef PBF_DIAG_SYNTH
+#define PBF_DIAG_SYNTH 0
+#endif
+#ifndef PBF_DIAG_GNOLOAD
+#define PBF_DIAG_GNOLOAD 0
+#endif
+#ifndef PBF_DIAG_GNOATOM
+#define PBF_DIAG_GNOATOM 0
+#endif
+#ifndef PBF_DIAG_FULL
+#define PBF_DIAG_FULL 0
+#endif
 #ifndef PBF_DIAG_SINK
 #define PBF_DIAG_SINK 0
 #endif
@@ -95,12 +110,8 @@ __device__ __forceinline__ uint32_t ring_pos(uint32_t h, const TileMap& tm) {
 // atomics of a key issue back to back.
 //
 // Per position the append is one LDS atomic (returns lim | tail), one compare, the slot address
-// (b << 7 | tail & 124, or the dump word) and one LDS store; per sub-chunk each thread flushes its
-// own tile: one LDS read of ht, and for a full group (16 entries) four 16-B LDS reads and four
-// 16-B stores to the region (the four stores of a group come from one lane in consecutive
-// instructions, so the L2 line is complete before it is written back).  (Round 4 listed the
-// complete groups of 64 tiles per wave with ballots and descriptors and wrote each group with
-// 4 lanes: ~45 VALU per thread and flush, against ~12 here.)
+// (b << 7 | tail & 124, or the dump word) and one LDS store (8 VALU with the tile and the entry);
+// per sub-chunk each thread flushes its own tile (take_groups / put_groups below).
 template <int KMAX, int KM, bool PROBE, bool POW2, bool EXACT>
 __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k, TileMap tm, PartGeom pg,
                                                     uint32_t* __restrict__ regions, uint32_t* __restrict__ fill,
@@ -163,7 +174,10 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
 #pragma unroll
             for (int u = 0; u < P; ++u) {
                 const uint64_t i = c0 + uint64_t(u) * kps + tid;
-                kw[u] = ld_stream_nt<kNtKeys>(reinterpret_cast<const uint32_t*>(ks.data) + min(i, n - 1) * 4);
+                if (PBF_DIAG_SYNTH)  // diagnostic: keys made in registers (no key loads)
+                    kw[u] = make_uint4(uint32_t(i) * 0x9E3779B1u, uint32_t(i) ^ 0x85EBCA6Bu, uint32_t(i >> 3) * 7u, uint32_t(i) + 12345u);
+                else
+                    kw[u] = ld_stream_nt<kNtKeys>(reinterpret_cast<const uint32_t*>(ks.data) + min(i, n - 1) * 4);
             }
         }
     };
@@ -174,10 +188,14 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
         if (x < pg.spill_cap) {
             sbuf[x * SW] = p;
             if constexpr (PROBE) sbuf[x * SW + 1] = uint32_t(i - k0);
-        } else if constexpr (PROBE) {
-            spill_probe(ps, pos_to_bit(p, tm), i);
         } else {
-            ovf[atomicAdd(ovf_count, 1u)] = p;
+            if constexpr (PROBE)
+                spill_probe(ps, pos_to_bit(p, tm), i);
+            else
+                ovf[atomicAdd(ovf_count, 1u)] = p;
+            // (rare) this path's global operations complete here, so the waits after the join
+            // can still count the flush stores of the common path instead of draining them
+            __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);
         }
     };
     // Group write-out, dense store instructions: the wave lists the groups its 64 tiles write
@@ -222,12 +240,23 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
         pd.x1 = *reinterpret_cast<const uint4*>(lds + RING0 + d1.x + q16);
         pd.a0 = d0.y + q16;
         pd.a1 = d1.y + q16;
+        if (PBF_DIAG_FULL) {  // diagnostic: every group written as its whole 128-B line (8 lanes)
+            for (uint32_t c = 0; c < 32; c += 8) {
+                const uint2 d = total ? wdesc[min(c + (lane >> 3), total - 1)] : dummy;
+                const uint32_t p16 = (lane & 7u) << 4;
+                const uint4 x = *reinterpret_cast<const uint4*>(lds + RING0 + (d.x & ~64u) + p16);
+                st_stream<NT>(reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(rgn) + ((d.y & ~127u) + p16)), x);
+            }
+        }
         for (uint32_t c = 32; c < total; c += 16) {
             const uint2 d = desc(c);
             const uint4 x = *reinterpret_cast<const uint4*>(lds + RING0 + d.x + q16);
             st_stream<NT>(reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(rgn) + (d.y + q16)), x);
         }
         __builtin_amdgcn_wave_barrier();
+    };
+    auto put_one = [&](uint32_t a, const uint4& x) {
+        if (!PBF_DIAG_NOSTORE) st_stream<NT>(reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(rgn) + (a & PBF_DIAG_WMASK)), x);
     };
     uint32_t diag_log = 0;
     uint4 diag_x = make_uint4(0, 0, 0, 0);
@@ -245,7 +274,7 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
             st_stream<NT>(reinterpret_cast<uint32_t*>(base + ((diag_log & 0xFFFF) + lane * 16)), pd.x0);
             st_stream<NT>(reinterpret_cast<uint32_t*>(base + (((diag_log + 1024) & 0xFFFF) + lane * 16)), pd.x1);
             diag_log += 2048;
-        } else if (!PBF_DIAG_NOSTORE) {
+        } else if (!PBF_DIAG_NOSTORE && !PBF_DIAG_FULL) {
             st_stream<NT>(reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(rgn) + (pd.a0 & PBF_DIAG_WMASK)), pd.x0);
             st_stream<NT>(reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(rgn) + (pd.a1 & PBF_DIAG_WMASK)), pd.x1);
         }
@@ -256,14 +285,23 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
         put_groups(pd);
     };
     uint32_t pos[KMAX];
-    auto hash_sub = [&](uint64_t s0, const uint4& w) {  // the positions of sub-chunk s0's key of this thread
+    // the positions of sub-chunk s0's key of this thread.  Fixed 16-byte keys are hashed by every
+    // lane (a lane past the keys hashes a clamped copy, never appended), so the pending flush's two
+    // stores can be issued between the seeds (PBF_SPREAD_STORES) rather than in one burst.
+    auto hash_sub = [&](uint64_t s0, const uint4& w, const Pending* pd) {
         const uint64_t i = s0 + tid;
-        if (tid < kps && i < k1) {
+        if constexpr (F16) {
+            auto emit = [&](int s, uint32_t h) {
+                pos[s] = ring_pos<POW2>(h, tm);
+                if (PBF_SPREAD_STORES && pd) {
+                    if (s == 1) put_one(pd->a0, pd->x0);
+                    if (s == KMAX - 2) put_one(pd->a1, pd->x1);
+                }
+            };
+            murmur_seeds16<KMAX>(w, k, emit);
+        } else if (tid < kps && i < k1) {
             auto emit = [&](int s, uint32_t h) { pos[s] = ring_pos<POW2>(h, tm); };
-            if constexpr (F16)
-                murmur_seeds16<KMAX>(w, k, emit);
-            else
-                hash_key<KMAX, KM>(ks, i, k, emit);
+            hash_key<KMAX, KM>(ks, i, k, emit);
         }
     };
     // the first batch's keys are taken before the loop; inside it a batch's keys are taken at the
@@ -274,7 +312,11 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
 #pragma unroll
         for (int u = 0; u < P; ++u) cw[u] = kw[u];
     }
-    hash_sub(k0, cw[0]);
+    hash_sub(k0, cw[0], nullptr);
+    // Nothing in flight at the loop's entry: otherwise the wait the compiler places at the loop
+    // header, merging the entry path (the first batch's second key load pending) with the back
+    // edge, is a full vmcnt(0) that drains every batch's flush stores
+    __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);
     uint32_t j = 0;  // sub-chunks done
     for (uint64_t c0 = k0; c0 < k1; c0 += uint64_t(P) * kps) {
         if (c0 + uint64_t(P) * kps < k1) load_batch(c0 + uint64_t(P) * kps);
@@ -335,16 +377,17 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
             }
             // the next sub-chunk's hash (the next batch's keys, at a batch's end), then this
             // flush's stores
+            constexpr bool spread = PBF_SPREAD_STORES && F16 && KMAX >= 3;
             if constexpr (u + 1 < P) {
-                hash_sub(s0 + kps, cw[F16 ? u + 1 : 0]);
+                hash_sub(s0 + kps, cw[F16 ? u + 1 : 0], spread ? &pd : nullptr);
             } else {
                 if constexpr (F16) {
 #pragma unroll
                     for (int x = 0; x < P; ++x) cw[x] = kw[x];
                 }
-                hash_sub(c0 + uint64_t(P) * kps, cw[0]);
+                hash_sub(c0 + uint64_t(P) * kps, cw[0], spread ? &pd : nullptr);
             }
-            put_groups(pd);
+            if constexpr (!spread) put_groups(pd);
             ++j;
         };
         static_assert(P == 2, "two sub-chunks per batch");
@@ -493,7 +536,7 @@ __device__ __forceinline__ void gather_ring_body(TileMap tm, PartGeom pg, uint64
                 }
 #pragma unroll
                 for (int u = 0; u < U; ++u)
-                    if (anyq[u]) v[u] = ld_stream(entries_at(b0 + u * nwaves, r0 + lane * 4));
+                    if (anyq[u]) v[u] = PBF_DIAG_GNOLOAD ? make_uint4(lane, r0, u, b0) : ld_stream(entries_at(b0 + u * nwaves, r0 + lane * 4));
             } else {
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
@@ -548,7 +591,10 @@ __device__ __forceinline__ void gather_ring_body(TileMap tm, PartGeom pg, uint64
                                 const uint32_t key = ((lo + uint32_t(r + t >= nxt1)) << 12) + (vv[t] >> kSlotShift);
 #pragma unroll
                                 for (int f = 0; f < NFM; ++f)
-                                    if ((fl[f] >> (8 * t)) & 1u) atomicAnd(kbits + f * kw + (key >> 5), ~(1u << (key & 31)));
+                                    if ((fl[f] >> (8 * t)) & 1u) {
+                                        if (PBF_DIAG_GNOATOM) kbits[(f * kw + (key >> 5)) & 7] = key;  // diagnostic
+                                        else atomicAnd(kbits + f * kw + (key >> 5), ~(1u << (key & 31)));
+                                    }
                             }
                         } else {
                             uint32_t nxt = nxt1;

@@ -49,6 +49,9 @@ constexpr bool kNtProbePart = true;   // probe partition's group stores
 constexpr bool kNtTileStore = true;   // k_tile_build's bitmap write-out
 constexpr bool kNtKeys = true;        // the partitions' 16-B key loads
 constexpr bool kNtTileLoad = false;   // bitmap loads into the LDS tiles
+#ifndef PBF_TILE_DMA
+#define PBF_TILE_DMA 1
+#endif
 // Regions of loads in flight per wave: the tile build 4, the tile test 8 words, the gather 4
 // (16 loads per wave in the tile test and 8 regions in the gather measured slower).
 constexpr int kTileBuildRegionsInFlight = 4;
@@ -148,6 +151,9 @@ __device__ __forceinline__ uint64_t tile_word0(uint32_t t, const TileMap& tm) {
 // Barrier for LDS hand-offs only: waits for this wave's LDS/scalar operations, not for its
 // global stores (which __syncthreads' workgroup-release fence would drain every time).
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+// s_waitcnt immediate (gfx9 encoding: vmcnt bits 3:0 and 15:14, expcnt 6:4, lgkmcnt 11:8) for
+// vmcnt(0) alone.  As a builtin (not inline asm) the compiler's own wait placement sees it.
+constexpr unsigned kWaitVmcnt0 = 0x0F70;
 
 // Block-wide exclusive scan of a[0..B) (LDS) into out[0..B] (LDS), out[B] = total.
 // blockDim a multiple of 64, <= 1024; warp_sums holds blockDim/64 entries.  Ends synced.
@@ -726,12 +732,28 @@ __device__ __forceinline__ void tile_probe_body(uint32_t* smem, uint32_t b, cons
     const uint64_t w0 = tile_word0(b, tm);
     const uint32_t nw = uint32_t(min<uint64_t>(W, tm.total_words - w0));
     const uint32_t tid = threadIdx.x, nt = blockDim.x;
-    for (uint32_t q = tid; q < G; q += nt) fills[q] = (fill[uint64_t(b) * G + q] + 31) >> 5;  // words
-    load_tile(tile, bitmap, w0, nw, W);
+    // The region fills are loaded (and waited for) first; then the bitmap tile goes global -> LDS by
+    // LDS-DMA while the word scan and the per-word table are built (no global load in between,
+    // which would wait for the DMA too), and the stream starts once the DMA has landed.  (G <=
+    // blockDim.x: thread q keeps region q's fill in a register.)
+    const bool dma = PBF_TILE_DMA && (w0 & 3) == 0 && nw == W && G <= nt;
+    uint32_t fq_own = 0;
+    if (dma) {
+        if (tid < G) fq_own = fill[uint64_t(b) * G + tid];
+        if (tid < G) fills[tid] = (fq_own + 31) >> 5;  // words (waits for the fill load only)
+        const uint32_t lane = tid & 63, wave = tid >> 6, nwaves = nt >> 6;
+        for (uint32_t c = wave; c < W / 256; c += nwaves)  // 1 KiB per wave instruction
+            __builtin_amdgcn_global_load_lds(
+                (const __attribute__((address_space(1))) void*)(bitmap + w0 + c * 256 + lane * 4),
+                (__attribute__((address_space(3))) void*)(tile + c * 256), 16, 0, 0);
+    } else {
+        for (uint32_t q = tid; q < G; q += nt) fills[q] = (fill[uint64_t(b) * G + q] + 31) >> 5;  // words
+        load_tile(tile, bitmap, w0, nw, W);
+    }
     lds_barrier();
     block_exclusive_scan(fills, wpre, G, ws);
     for (uint32_t q = tid; q < G; q += nt) {
-        const uint32_t fq = fill[uint64_t(b) * G + q];
+        const uint32_t fq = dma ? fq_own : fill[uint64_t(b) * G + q];
         fills[q] = fq;  // entries again
         if constexpr (TAB == 2) {
             const uint32_t base = uint32_t(region_id(q, b, G, B)) * wpr;
@@ -744,6 +766,7 @@ __device__ __forceinline__ void tile_probe_body(uint32_t* smem, uint32_t b, cons
             for (uint32_t c = wpre[q]; c < wpre[q + 1]; ++c) wq[c] = uint16_t(q);
         }
     }
+    if (dma) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's tile pieces landed
     lds_barrier();
     const uint32_t total = wpre[G];
     const uint32_t lane = tid & 63, wave = tid >> 6, nwaves = nt >> 6;

@@ -41,6 +41,9 @@ def test_one_key_may_contain_matches_oracle(oracle):
         got = [bf.may_contain(s) for s in probes]
         assert got == [bool(x) for x in want_hm[:len(probes)]], (nb, k)
         assert bf.last_probe_detail & _native.PBF_DETAIL_ONE_KEY or len(probes[-1]) > 4096
+        if k <= 32:  # a short key of a built filter: the resident reader answered (no launch)
+            assert bf.may_contain(keys[0])
+            assert bf.last_probe_detail & _native.PBF_DETAIL_RESIDENT
 
 
 def test_reader_threads_share_one_filter(oracle):
@@ -220,7 +223,67 @@ def test_shared_readers_beside_a_writer_on_the_same_filter(oracle):
     w.join(timeout=300)
     assert not errors, errors[:5]
     assert bf.bitmap() == want.tobytes()
-    assert bf.may_contain(qs[0]) == bool(wb[0]) and bf.last_probe_detail == _native.PBF_DETAIL_ONE_KEY
+    assert bf.may_contain(qs[0]) == bool(wb[0])
+    # a built, idle filter: the one-key probe ran under the shared lock, answered by the
+    # resident reader wave
+    assert bf.last_probe_detail == (_native.PBF_DETAIL_ONE_KEY | _native.PBF_DETAIL_SHARED
+                                    | _native.PBF_DETAIL_RESIDENT)
+
+
+def test_shared_readers_see_keys_a_writer_added(oracle):
+    """Round-4 advice: a writer adds NEW keys (bits change) and then signals; reader threads then
+    probe those keys and must all hit — whether their call finds the add still queued on the
+    filter's stream (the exclusive path, ordered after it) or finished (the shared path)."""
+    n0, n1 = 50_000, 20_000
+    bf = BloomFilter(2 ** 18, 6)
+    bf.add_many(PackedKeys.fixed(splitmix_hex_keys(91, 0, n0)))
+    bf.sync()
+    new = _strs(PackedKeys.fixed(splitmix_hex_keys(91, n0, n1)))
+    rounds = 6
+    added = [threading.Event() for _ in range(rounds)]
+    errors = []
+
+    def writer():
+        for r in range(rounds):
+            bf.add_many(new[r * (n1 // rounds):(r + 1) * (n1 // rounds)])
+            added[r].set()
+
+    def reader(t):
+        try:
+            for r in range(rounds):
+                added[r].wait(timeout=120)
+                for i in range(r * (n1 // rounds) + t, (r + 1) * (n1 // rounds), 97):
+                    if not bf.may_contain(new[i]):
+                        errors.append((t, r, i))
+                        return
+        except Exception as e:  # pragma: no cover
+            errors.append(("exc", t, repr(e)))
+
+    th = [threading.Thread(target=reader, args=(t,)) for t in range(8)]
+    for t in th:
+        t.start()
+    w = threading.Thread(target=writer)
+    w.start()
+    w.join(timeout=300)
+    for t in th:
+        t.join(timeout=300)
+    assert not errors, errors[:5]
+    want = oracle.build(2 ** 18, 6, PackedKeys.fixed(splitmix_hex_keys(91, 0, n0 + (n1 // rounds) * rounds)))
+    assert bf.bitmap() == want.tobytes()
+
+
+def test_one_key_probe_exclusive_fallback_in_a_subprocess():
+    """PBF_SHARED_READERS=0 sends one-key probes through the exclusive path: the handle records
+    the one-key launch without the shared flag (the same answers)."""
+    code = ("import sys; sys.path.insert(0, '.'); from pebbledb_amd import BloomFilter, _native\n"
+            "bf = BloomFilter(4096, 4); bf.add('a'); bf.sync()\n"
+            "assert bf.may_contain('a')\n"
+            "print(bf.last_probe_detail == _native.PBF_DETAIL_ONE_KEY)")
+    env = dict(os.environ, PBF_SHARED_READERS="0")
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300, cwd=repo)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout.strip().splitlines()[-1] == "True"
 
 
 def test_wait_stream_orders_a_torch_producer_without_sync(oracle):
@@ -260,3 +323,87 @@ def test_wait_stream_orders_a_torch_producer_without_sync(oracle):
     want_hm = oracle.probe(want, 6, PackedKeys.fixed(splitmix_hex_keys(31, n // 2, n)))
     assert np.array_equal(copy.cpu().numpy(), want_hm)
     bf.sync()
+
+
+def _run_py(code: str, env_extra: dict) -> str:
+    env = dict(os.environ, **env_extra)
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300, cwd=REPO)
+    assert r.returncode == 0, r.stderr[-2000:]
+    return r.stdout.strip().splitlines()[-1]
+
+
+def test_resident_reader_off_launches_per_key_in_a_subprocess():
+    """PBF_RESIDENT_READER=0: the shared one-key probe launches per key (no resident flag), with
+    the same answers."""
+    code = ("import sys; sys.path.insert(0, '.'); from pebbledb_amd import BloomFilter, _native\n"
+            "bf = BloomFilter(4096, 4); bf.add_many(['a', 'b']); bf.sync()\n"
+            "assert bf.may_contain('a') and bf.may_contain('b')\n"
+            "print(bf.last_probe_detail == _native.PBF_DETAIL_ONE_KEY | _native.PBF_DETAIL_SHARED)")
+    assert _run_py(code, {"PBF_RESIDENT_READER": "0"}) == "True"
+
+
+def test_resident_reader_relaunches_after_idle_in_a_subprocess():
+    """With a 50 us idle time the resident wave leaves between keys separated by 2 ms sleeps and
+    is relaunched by the next key: every answer still equals the per-key launch's, and the wave
+    was started more than once."""
+    code = textwrap.dedent("""
+        import sys, time, ctypes; sys.path.insert(0, '.')
+        from pebbledb_amd import BloomFilter, _native
+        from pebbledb_amd.keys import splitmix_hex_keys_str
+        keys = splitmix_hex_keys_str(7, 0, 2000)
+        bf = BloomFilter(2 ** 12, 5); bf.add_many(keys); bf.sync()
+        probes = splitmix_hex_keys_str(7, 1000, 200)
+        got = []
+        for i, p in enumerate(probes):
+            got.append(bf.may_contain(p))
+            assert bf.last_probe_detail & _native.PBF_DETAIL_RESIDENT
+            if i % 20 == 0:
+                time.sleep(0.002)
+        n = ctypes.c_uint32(0)
+        _native.check(_native.lib().pbf_resident_launches(bf.device, ctypes.byref(n)))
+        print(n.value, ''.join('1' if g else '0' for g in got))
+    """)
+    out = _run_py(code, {"PBF_RESIDENT_IDLE_US": "50"})
+    launches, bits = out.split()
+    code0 = textwrap.dedent("""
+        import sys; sys.path.insert(0, '.')
+        from pebbledb_amd import BloomFilter
+        from pebbledb_amd.keys import splitmix_hex_keys_str
+        keys = splitmix_hex_keys_str(7, 0, 2000)
+        bf = BloomFilter(2 ** 12, 5); bf.add_many(keys); bf.sync()
+        print(''.join('1' if bf.may_contain(p) else '0' for p in splitmix_hex_keys_str(7, 1000, 200)))
+    """)
+    assert _run_py(code0, {"PBF_RESIDENT_READER": "0"}) == bits
+    assert bits == "1" * 200  # probes are keys 1000..1199 of the 2000 members
+    assert int(launches) >= 2
+
+
+def test_more_threads_than_resident_slots(oracle):
+    """80 threads probe one filter at once: the first 64 hold resident slots, the rest launch per
+    key; every answer equals the oracle's."""
+    n = 20_000
+    pk = PackedKeys.fixed(splitmix_hex_keys(17, 0, n))
+    bf = BloomFilter(2 ** 15, 6)
+    bf.add_many(pk)
+    bf.sync()
+    want = np.unpackbits(oracle.probe(oracle.build(2 ** 15, 6, pk), 6, pk), bitorder="little")[:n]
+    qs = _strs(pk)
+    errors = []
+    barrier = threading.Barrier(80)
+
+    def reader(t):
+        try:
+            barrier.wait(timeout=120)
+            for i in range(t, n, 397):
+                if bf.may_contain(qs[i]) != bool(want[i]):
+                    errors.append((t, i))
+                    return
+        except Exception as e:  # pragma: no cover
+            errors.append(("exc", t, repr(e)))
+
+    th = [threading.Thread(target=reader, args=(t,)) for t in range(80)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    assert not errors, errors[:5]

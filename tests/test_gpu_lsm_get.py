@@ -155,4 +155,5 @@ def test_per_key_get_one_launch_equals_reference_lsm_get_golden():
     g, l0, levels = _golden_store()
     for key, want in zip(g["probes"], g["order"]):
         assert candidates_one(key, l0, levels) == want, key
-    assert l0[0].last_probe_detail == _native.PBF_DETAIL_ONE_KEY | _native.PBF_DETAIL_SET
+    assert l0[0].last_probe_detail == (_native.PBF_DETAIL_ONE_KEY | _native.PBF_DETAIL_SET
+                                       | _native.PBF_DETAIL_RESIDENT)

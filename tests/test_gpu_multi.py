@@ -398,3 +398,35 @@ def test_multi_placement_groups_one_thread_each(oracle):
         assert np.array_equal(gv[i], oracle.probe(want[i], kk[i], vq)), i
     with pytest.raises(ValueError):
         may_contain_multi([fs[0], fs[0]], q, groups=[0, 1])  # a filter twice
+
+
+def _device_count():
+    try:
+        import torch
+        return torch.cuda.device_count()
+    except Exception:  # pragma: no cover
+        return 0
+
+
+@pytest.mark.skipif(_device_count() < 2, reason="needs two GPUs (the driver's multi-GPU node)")
+def test_filters_on_two_devices_from_one_process(oracle):
+    """Round-4 advice: the cross-device fan-out with filters REALLY on two devices — a host batch
+    against filters on devices 0 and 1 (by device: one host thread per device; with explicit
+    groups; and the one-key set probe, one launch per device) equals the oracle."""
+    nb, k, n_per = 2 ** 20, 6, 30_000
+    fs, want = [], []
+    for i in range(6):
+        keys = PackedKeys.fixed(splitmix_hex_keys(SEED, i * n_per, n_per))
+        bf = BloomFilter(nb, k, device=i % 2)
+        bf.add_many(keys)
+        fs.append(bf)
+        want.append(oracle.build(nb, k, keys))
+    assert {bf.device for bf in fs} == {0, 1}
+    q = PackedKeys.fixed(splitmix_hex_keys(SEED, n_per // 2, 6 * n_per))
+    for got in (may_contain_multi(fs, q), may_contain_multi(fs, q, groups=[0, 1, 2, 3, 2, 3])):
+        for i in range(len(fs)):
+            assert np.array_equal(got[i], oracle.probe(want[i], k, q)), i
+    qs = [bytes(x).decode() for x in splitmix_hex_keys(SEED, n_per - 50, 100)]
+    for key in qs:
+        exp = [bool(np.unpackbits(oracle.probe(w, k, PackedKeys.from_strs([key])), bitorder="little")[0]) for w in want]
+        assert may_contain_set(fs, key) == exp

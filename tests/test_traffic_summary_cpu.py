@@ -51,3 +51,17 @@ def test_committed_traffic_matches_the_sources():
         assert t["source_sha256"] == source_digest(), cfg
         assert t["passes"]["build"]["traffic_bytes"] > 0 and t["passes"]["probe"]["traffic_bytes"] > 0
     assert pass_of("pbf::k_tile_build<true>") == "build"
+
+
+def test_every_pass_kernel_has_a_calibrated_read_shape():
+    """Each kernel of a timed pass is mapped to the load shape its FETCH_SIZE factor was
+    calibrated on (fetch_cal.hip, profiles/r05/ab/summary.md), not a default."""
+    from traffic_summary import CALIBRATION, KERNEL_SHAPE, read_factor
+    for name in ("pbf::k_part_ring<6, 0, true, true, true>", "pbf::k_part<8, 2, true>", "pbf::k_tile_build<true>",
+                 "pbf::k_ovf_build", "pbf::k_tile_probe<2>", "pbf::k_tile_probe_set<2>", "pbf::k_gather_ring<1>",
+                 "pbf::k_gather_ring<8>", "pbf::k_hw_to_hitmask"):
+        base = name.replace("pbf::", "").split("<")[0]
+        assert base in KERNEL_SHAPE, name
+        shape, factor = read_factor(name)
+        assert shape in CALIBRATION and factor == CALIBRATION[shape]
+    assert all(abs(f - 2.0) < 0.01 for f in CALIBRATION.values())

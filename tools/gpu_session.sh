@@ -83,6 +83,11 @@ for step in "$@"; do
     prof_c5) prof prof_c5 600 --config c5 --steps 3 --warmup 1 --no-cpu-baseline --no-host-c5 ;;
     ab) ab ab 300 2 --steps 50 --warmup 5 ;;
     ab1) ab ab 300 1 --steps 50 --warmup 5 ;;
+    c5sim) for lay in keys filters; do
+             run c5sim_${lay}_w8 600 python bench.py --config c5 --sim-world 8 --sim-rank 0 --c5-layout $lay --steps 5 --warmup 2 --no-host-c5 --no-cpu-baseline --no-compare
+             run c5sim_${lay}_w2 600 python bench.py --config c5 --sim-world 2 --sim-rank 0 --c5-layout $lay --steps 5 --warmup 2 --no-host-c5 --no-cpu-baseline --no-compare
+           done ;;
+    c4sim) run c4sim_w8 600 python bench.py --config c4 --sim-world 8 --sim-rank 0 --steps 3 --warmup 1 --no-cpu-baseline ;;
     profab) prof profq_default 300 --steps 20 --warmup 5 --no-cpu-baseline --no-host-inclusive
             for v in build/variants/*.so; do
               nm=$(basename $v .so)

@@ -6,8 +6,14 @@ FETCH_SIZE and WRITE_SIZE come from separate `--pmc` runs of the same short benc
 group per run: FETCH_SIZE uses 3 of the 4 TCC slots, WRITE_SIZE 2).  Both are in KiB.  Per
 MI355X_MICROARCH.md §HBM, on gfx950 FETCH_SIZE reports exactly half the bytes of a wide
 (16 B/lane) streaming read, so fetched bytes = 2 x FETCH_SIZE x 1024; WRITE_SIZE is exact for
-16-B-per-lane stores.  Every kernel of the bloom passes reads its streams 16 B per lane
-(keys, region entries); the random word reads of the probe's spill path are negligible.
+16-B-per-lane stores.
+
+The factor is calibrated per access shape (tools/microbench/fetch_cal.hip, record
+profiles/r05/ab/summary.md "FETCH_SIZE calibration"): a 1 GiB buffer read once with each load
+shape the bloom kernels use — 16 B per lane non-temporal and temporal, 16 B per lane on every
+other 64-B quad, 4 B per lane with 8 lanes per word, 4 B per lane contiguous — reported
+FETCH_SIZE = 524,298-524,300 KiB each, i.e. a factor of 2.000 for every shape.  READ_FACTOR maps
+each kernel to the shape of its HBM reads and that shape's measured factor.
 
 Per kernel the median over dispatches of the full-size launches is taken; a pass's traffic is
 the sum over its kernels.  A pass split into several pipelines (C3's probe: 200M keys in two
@@ -21,6 +27,34 @@ import collections
 import csv
 import json
 import sys
+
+# bytes / (FETCH_SIZE x 1024) measured per load shape (fetch_cal.hip, MI355X, round 5)
+CALIBRATION = {
+    "16B_lane_nt": 2.000,       # k_cal_read16
+    "16B_lane": 2.000,          # k_cal_read16_t
+    "16B_lane_half_lines": 2.000,  # k_cal_read16_q: the whole 128-B line is fetched
+    "4B_lane_shared_word": 2.000,  # k_cal_read4_w
+    "4B_lane": 2.000,           # k_cal_read4
+}
+# the shape of each kernel's dominant HBM reads
+KERNEL_SHAPE = {
+    "k_part_ring": "16B_lane_nt",      # 16-B key loads
+    "k_part": "16B_lane_nt",
+    "k_tile_build": "16B_lane_nt",     # region words, packed entries
+    "k_ovf_build": "4B_lane",
+    "k_tile_probe": "16B_lane_nt",     # region words (LDS-DMA or 16-B loads) + bitmap tile
+    "k_tile_probe_set": "16B_lane",    # temporal: a set's workgroups share lines
+    "k_gather_ring": "16B_lane_half_lines",  # failed quads' entries; result words 4 B / lane
+    "k_gather": "16B_lane_half_lines",
+    "k_hw_to_hitmask": "4B_lane",
+}
+
+
+def read_factor(kernel: str) -> tuple[str, float]:
+    base = kernel.replace("pbf::", "").split("<")[0]
+    shape = KERNEL_SHAPE.get(base, "16B_lane")
+    return shape, CALIBRATION[shape]
+
 
 PASSES = {
     "build": ("k_part_ring<", "false", "k_part<", "k_tile_build", "k_ovf_build"),
@@ -66,15 +100,19 @@ def main() -> None:
     fetch = per_kernel(fdir, "FETCH_SIZE")
     write = per_kernel(wdir, "WRITE_SIZE")
     res = {"config": config, "source": f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE ({fdir}, {wdir})",
-           "correction": "read bytes = 2 x FETCH_SIZE x 1024 (gfx950 wide-read halving), write bytes = WRITE_SIZE x 1024",
+           "correction": "read bytes = factor(shape) x FETCH_SIZE x 1024 (gfx950 read halving, calibrated per load "
+                         "shape), write bytes = WRITE_SIZE x 1024",
+           "calibration": {"record": "profiles/r05/ab/summary.md (FETCH_SIZE calibration; tools/microbench/fetch_cal.hip)",
+                           "factors": CALIBRATION},
            "kernels": {}, "passes": {}}
     for k in sorted(set(fetch) | set(write)):
         p = pass_of(k)
         if p is None:
             continue
-        rd = 2.0 * fetch.get(k, 0.0) * 1024
+        shape, factor = read_factor(k)
+        rd = factor * fetch.get(k, 0.0) * 1024
         wr = write.get(k, 0.0) * 1024
-        res["kernels"][k] = {"pass": p, "read_bytes": rd, "write_bytes": wr}
+        res["kernels"][k] = {"pass": p, "read_bytes": rd, "write_bytes": wr, "read_shape": shape, "read_factor": factor}
         agg = res["passes"].setdefault(p, {"read_bytes": 0.0, "write_bytes": 0.0})
         agg["read_bytes"] += rd
         agg["write_bytes"] += wr
