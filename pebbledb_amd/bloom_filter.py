@@ -198,15 +198,19 @@ class BloomFilter:
             self._flush()
 
     def may_contain(self, key: str) -> bool:
-        """bloom_filter.py:67-74 — one key, one kernel launch (pbf_may_contain)."""
-        if not self._require_modulus():
-            return True  # k == 0: the AND over no bits
+        """bloom_filter.py:67-74 for one key (pbf_may_contain: answered by the device's resident
+        reader wave, or one launch)."""
+        if self.nb_hash_functions <= 0 or self.nb_bytes <= 0:
+            if not self._require_modulus():
+                return True  # k == 0: the AND over no bits
         if self._pending:
             self._flush()
         out = ctypes.c_int(0)
         enc = key.encode("utf-8")
-        _native.check(_native.lib().pbf_may_contain(self._h, enc, len(enc), ctypes.byref(out)), "pbf_may_contain")
-        return bool(out.value)
+        rc = _native.lib().pbf_may_contain(self._h, enc, len(enc), ctypes.byref(out))
+        if rc:
+            _native.check(rc, "pbf_may_contain")
+        return out.value != 0
 
     def to_bytes(self) -> bytes:
         """bloom_filter.py:76-81: little-endian bitmap + one byte of k (struct.error if k > 255)."""
@@ -423,12 +427,23 @@ def may_contain_set(filters, key: str) -> list[bool]:
     (src/lsm_storage.py:164-179).  Filters may have any sizes; filters on several devices take
     one launch per device."""
     filters = list(filters)
-    if not filters:
+    nf = len(filters)
+    if not nf:
         return []
-    native = _native_set(filters)
-    res = [True] * len(filters)  # k == 0: the AND over no bits
     enc = key.encode("utf-8")
-    for dev in dict.fromkeys(filters[i].device for i in native):  # one launch per device
+    # the common shape (LsmStorage.get: built filters, k > 0, one device): one call, no numpy
+    dev0 = filters[0].device
+    if all(bf.nb_hash_functions > 0 and bf.nb_bytes > 0 and not bf._pending and bf.device == dev0 for bf in filters):
+        hs = (ctypes.c_void_p * nf)(*[bf._h.value for bf in filters])
+        out = (ctypes.c_uint8 * ((nf + 7) // 8))()
+        rc = _native.lib().pbf_may_contain_set(hs, nf, enc, len(enc), out)
+        if rc:
+            _native.check(rc, "pbf_may_contain_set")
+        bits = int.from_bytes(bytes(out), "little")
+        return [(bits >> j) & 1 == 1 for j in range(nf)]
+    native = _native_set(filters)
+    res = [True] * nf  # k == 0: the AND over no bits
+    for dev in dict.fromkeys(filters[i].device for i in native):  # one call per device
         idx = [i for i in native if filters[i].device == dev]
         hs = (ctypes.c_void_p * len(idx))(*[filters[i]._h.value for i in idx])
         out = np.zeros((len(idx) + 7) // 8, dtype=np.uint8)

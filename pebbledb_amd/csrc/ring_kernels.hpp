@@ -49,6 +49,14 @@ static_assert(kSlotShift == 20 && kRingKeysPerSub == 1024 && kGroupKeys == 4 * k
 // Key sub-chunks loaded per batch, one batch ahead: 2 measured best with the non-temporal streams
 // (C2 A/B over 1/2/3/4/8: profiles/r01/s11/ab.txt)
 constexpr int kRingPrefetch = 2;
+#ifndef PBF_RING_BFE
+#define PBF_RING_BFE 1
+#endif
+constexpr bool kRingBfe = PBF_RING_BFE;  // tile of a power-of-two position by one bit-field extract
+#ifndef PBF_GATHER_BRANCH_FREE
+#define PBF_GATHER_BRANCH_FREE 1
+#endif
+constexpr bool kGatherBranchFree = PBF_GATHER_BRANCH_FREE;
 #ifndef PBF_DIAG_NOSTORE
 #define PBF_DIAG_NOSTORE 0
 #endif
@@ -284,7 +292,14 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
         take_groups(has, hb, pd);
         put_groups(pd);
     };
+    // pos[s]: with a power-of-two m the raw hash (its tile is one bit-field extract, the entry
+    // keeps the low tb bits), else the position in [0, m)
     uint32_t pos[KMAX];
+    const uint32_t bbits = 31u - __builtin_clz(B | 1u);  // log2 B (B a power of two when POW2)
+    auto tile_of = [&](uint32_t p) {
+        if constexpr (POW2 && kRingBfe) return __builtin_amdgcn_ubfe(p, shift, bbits);
+        return p >> shift;
+    };
     // the positions of sub-chunk s0's key of this thread.  Fixed 16-byte keys are hashed by every
     // lane (a lane past the keys hashes a clamped copy, never appended), so the pending flush's two
     // stores can be issued between the seeds (PBF_SPREAD_STORES) rather than in one burst.
@@ -292,7 +307,7 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
         const uint64_t i = s0 + tid;
         if constexpr (F16) {
             auto emit = [&](int s, uint32_t h) {
-                pos[s] = ring_pos<POW2>(h, tm);
+                pos[s] = POW2 && kRingBfe ? h : ring_pos<POW2>(h, tm);
                 if (PBF_SPREAD_STORES && pd) {
                     if (s == 1) put_one(pd->a0, pd->x0);
                     if (s == KMAX - 2) put_one(pd->a1, pd->x1);
@@ -300,7 +315,7 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
             };
             murmur_seeds16<KMAX>(w, k, emit);
         } else if (tid < kps && i < k1) {
-            auto emit = [&](int s, uint32_t h) { pos[s] = ring_pos<POW2>(h, tm); };
+            auto emit = [&](int s, uint32_t h) { pos[s] = POW2 && kRingBfe ? h : ring_pos<POW2>(h, tm); };
             hash_key<KMAX, KM>(ks, i, k, emit);
         }
     };
@@ -333,13 +348,13 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
                 uint32_t v[KMAX];
 #pragma unroll
                 for (int s = 0; s < KMAX; ++s)
-                    if (s < k) v[s] = atomicAdd(ht + (pos[s] >> shift), 4u);
+                    if (s < k) v[s] = atomicAdd(ht + tile_of(pos[s]), 4u);
                 const uint32_t tag = PROBE ? (((j & 3u) << 30) | (tid << kSlotShift)) : 0u;
                 bool bad = false;  // a position overran its tile's ring or region
 #pragma unroll
                 for (int s = 0; s < KMAX; ++s) {
                     if (s < k) {
-                        const uint32_t b = pos[s] >> shift;
+                        const uint32_t b = tile_of(pos[s]);
                         const bool ok = (v[s] & 0xFFFFu) < (v[s] >> 16);
                         // every lane stores (a position that left the stream into the dump word):
                         // no per-seed exec-mask branch
@@ -351,7 +366,7 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
                 if (bad) {  // rare: heavy key duplication
 #pragma unroll
                     for (int s = 0; s < KMAX; ++s)
-                        if (s < k && (v[s] & 0xFFFFu) >= (v[s] >> 16)) spill_one(pos[s], i);
+                        if (s < k && (v[s] & 0xFFFFu) >= (v[s] >> 16)) spill_one(POW2 && kRingBfe ? pos[s] & tm.im.mask : pos[s], i);
                 }
             }
             lds_barrier();
@@ -589,12 +604,18 @@ __device__ __forceinline__ void gather_ring_body(TileMap tm, PartGeom pg, uint64
                             for (int t = 0; t < 4; ++t) {
                                 // key = 4096 group + key-in-group (the entry's top 12 bits)
                                 const uint32_t key = ((lo + uint32_t(r + t >= nxt1)) << 12) + (vv[t] >> kSlotShift);
+                                if constexpr (NFM == 1 && kGatherBranchFree) {
+                                    // every entry's LDS AND, a passing one's with all ones (no
+                                    // per-entry branch; most entries of a failed quad failed)
+                                    atomicAnd(kbits + (key >> 5), ~(((fl[0] >> (8 * t)) & 1u) << (key & 31)));
+                                } else {
 #pragma unroll
-                                for (int f = 0; f < NFM; ++f)
-                                    if ((fl[f] >> (8 * t)) & 1u) {
-                                        if (PBF_DIAG_GNOATOM) kbits[(f * kw + (key >> 5)) & 7] = key;  // diagnostic
-                                        else atomicAnd(kbits + f * kw + (key >> 5), ~(1u << (key & 31)));
-                                    }
+                                    for (int f = 0; f < NFM; ++f)
+                                        if ((fl[f] >> (8 * t)) & 1u) {
+                                            if (PBF_DIAG_GNOATOM) kbits[(f * kw + (key >> 5)) & 7] = key;  // diagnostic
+                                            else atomicAnd(kbits + f * kw + (key >> 5), ~(1u << (key & 31)));
+                                        }
+                                }
                             }
                         } else {
                             uint32_t nxt = nxt1;

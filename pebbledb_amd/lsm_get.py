@@ -104,12 +104,18 @@ def candidates_one(key: str, level0: Sequence[BloomFilter], levels: Sequence[Seq
     (lsm_storage.py:164-179), numbered as ``candidate_masks`` rows: L0 filters (newest first)
     and the level filters whose ``first_key <= key <= last_key`` (:173) are tested together in
     one ``pbf_may_contain_set`` launch."""
-    flat = [t for lvl in levels for t in lvl]
-    in_range = [j for j, t in enumerate(flat) if t.first_key <= key <= t.last_key]
-    tested = list(level0) + [flat[j].bloom_filter for j in in_range]
+    n0 = len(level0)
+    in_range, tested = [], list(level0)
+    j = 0
+    for lvl in levels:
+        for t in lvl:
+            if t.first_key <= key <= t.last_key:
+                in_range.append(j)
+                tested.append(t.bloom_filter)
+            j += 1
     if not tested:
         return []
     hits = may_contain_set(tested, key)
-    out = [t for t in range(len(level0)) if hits[t]]
-    out += [len(level0) + j for r, j in enumerate(in_range) if hits[len(level0) + r]]
+    out = [t for t in range(n0) if hits[t]]
+    out += [n0 + j for r, j in enumerate(in_range) if hits[n0 + r]]
     return out
