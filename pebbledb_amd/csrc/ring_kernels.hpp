@@ -57,39 +57,6 @@ constexpr bool kRingBfe = PBF_RING_BFE;  // tile of a power-of-two position by o
 #define PBF_GATHER_BRANCH_FREE 1
 #endif
 constexpr bool kGatherBranchFree = PBF_GATHER_BRANCH_FREE;
-#ifndef PBF_DIAG_NOSTORE
-#define PBF_DIAG_NOSTORE 0
-#endif
-#ifndef PBF_DIAG_WMASK
-#define PBF_DIAG_WMASK 0xFFFFFFFFu
-#endif
-#ifndef PBF_SPREAD_STORES
-#define PBF_SPREAD_STORES 0
-#endif
-#ifndef PBF_DIAG_SYNTH
-#define PBF_DIAG_SYNTH 0
-#endif
-#ifndef PBF_DIAG_GNOLOAD
-#define PBF_DIAG_GNOLOAD 0
-#endif
-#ifndef PBF_DIAG_GNOATOM
-#define PBF_DIAG_GNOATOM 0
-#endif
-#ifndef PBF_DIAG_FULL
-#define PBF_DIAG_FULL 0
-#endif
-#ifndef PBF_DIAG_SINK
-#define PBF_DIAG_SINK 0
-#endif
-#ifndef PBF_DIAG_CONST
-#define PBF_DIAG_CONST 0
-#endif
-#ifndef PBF_DIAG_LOG
-#define PBF_DIAG_LOG 0
-#endif
-#ifndef PBF_DIAG_NOAPPEND
-#define PBF_DIAG_NOAPPEND 0
-#endif
 // Region capacity bound of the ring partition: tail (bytes) must stay below 2^16 although a
 // sub-chunk may append up to kps * k <= 8192 positions past lim (all to one tile: a duplicated
 // key) before the flush clamps it: 4 * (cap + 8192) < 2^16.
@@ -182,10 +149,7 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
 #pragma unroll
             for (int u = 0; u < P; ++u) {
                 const uint64_t i = c0 + uint64_t(u) * kps + tid;
-                if (PBF_DIAG_SYNTH)  // diagnostic: keys made in registers (no key loads)
-                    kw[u] = make_uint4(uint32_t(i) * 0x9E3779B1u, uint32_t(i) ^ 0x85EBCA6Bu, uint32_t(i >> 3) * 7u, uint32_t(i) + 12345u);
-                else
-                    kw[u] = ld_stream_nt<kNtKeys>(reinterpret_cast<const uint32_t*>(ks.data) + min(i, n - 1) * 4);
+                kw[u] = ld_stream_nt<kNtKeys>(reinterpret_cast<const uint32_t*>(ks.data) + min(i, n - 1) * 4);
             }
         }
     };
@@ -248,14 +212,6 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
         pd.x1 = *reinterpret_cast<const uint4*>(lds + RING0 + d1.x + q16);
         pd.a0 = d0.y + q16;
         pd.a1 = d1.y + q16;
-        if (PBF_DIAG_FULL) {  // diagnostic: every group written as its whole 128-B line (8 lanes)
-            for (uint32_t c = 0; c < 32; c += 8) {
-                const uint2 d = total ? wdesc[min(c + (lane >> 3), total - 1)] : dummy;
-                const uint32_t p16 = (lane & 7u) << 4;
-                const uint4 x = *reinterpret_cast<const uint4*>(lds + RING0 + (d.x & ~64u) + p16);
-                st_stream<NT>(reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(rgn) + ((d.y & ~127u) + p16)), x);
-            }
-        }
         for (uint32_t c = 32; c < total; c += 16) {
             const uint2 d = desc(c);
             const uint4 x = *reinterpret_cast<const uint4*>(lds + RING0 + d.x + q16);
@@ -263,29 +219,9 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
         }
         __builtin_amdgcn_wave_barrier();
     };
-    auto put_one = [&](uint32_t a, const uint4& x) {
-        if (!PBF_DIAG_NOSTORE) st_stream<NT>(reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(rgn) + (a & PBF_DIAG_WMASK)), x);
-    };
-    uint32_t diag_log = 0;
-    uint4 diag_x = make_uint4(0, 0, 0, 0);
     auto put_groups = [&](const Pending& pd) {
-        if (PBF_DIAG_SINK) {  // diagnostic: no stores, the ring reads kept (their data folded into one word)
-            diag_x.x ^= pd.x0.x ^ pd.x1.y ^ pd.a0;
-            diag_x.y ^= pd.x0.y ^ pd.x1.z ^ pd.a1;
-            diag_x.z ^= pd.x0.z ^ pd.x1.w;
-            diag_x.w ^= pd.x0.w ^ pd.x1.x;
-        } else if (PBF_DIAG_CONST) {  // diagnostic: the stores without the ring reads' data
-            st_stream<NT>(reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(rgn) + pd.a0), make_uint4(pd.a0, 1, 2, 3));
-            st_stream<NT>(reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(rgn) + pd.a1), make_uint4(pd.a1, 1, 2, 3));
-        } else if (PBF_DIAG_LOG) {  // diagnostic: the same bytes as one contiguous log per wave
-            char* base = reinterpret_cast<char*>(rgn) + (uint32_t(wave) << 16);
-            st_stream<NT>(reinterpret_cast<uint32_t*>(base + ((diag_log & 0xFFFF) + lane * 16)), pd.x0);
-            st_stream<NT>(reinterpret_cast<uint32_t*>(base + (((diag_log + 1024) & 0xFFFF) + lane * 16)), pd.x1);
-            diag_log += 2048;
-        } else if (!PBF_DIAG_NOSTORE && !PBF_DIAG_FULL) {
-            st_stream<NT>(reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(rgn) + (pd.a0 & PBF_DIAG_WMASK)), pd.x0);
-            st_stream<NT>(reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(rgn) + (pd.a1 & PBF_DIAG_WMASK)), pd.x1);
-        }
+        st_stream<NT>(reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(rgn) + pd.a0), pd.x0);
+        st_stream<NT>(reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(rgn) + pd.a1), pd.x1);
     };
     auto write_groups = [&](bool has, uint32_t hb) {
         Pending pd;
@@ -301,18 +237,12 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
         return p >> shift;
     };
     // the positions of sub-chunk s0's key of this thread.  Fixed 16-byte keys are hashed by every
-    // lane (a lane past the keys hashes a clamped copy, never appended), so the pending flush's two
-    // stores can be issued between the seeds (PBF_SPREAD_STORES) rather than in one burst.
-    auto hash_sub = [&](uint64_t s0, const uint4& w, const Pending* pd) {
+    // lane (a lane past the keys hashes a clamped copy, never appended).  (Issuing the pending
+    // flush's two stores between the seeds instead of after the hash measured no different.)
+    auto hash_sub = [&](uint64_t s0, const uint4& w) {
         const uint64_t i = s0 + tid;
         if constexpr (F16) {
-            auto emit = [&](int s, uint32_t h) {
-                pos[s] = POW2 && kRingBfe ? h : ring_pos<POW2>(h, tm);
-                if (PBF_SPREAD_STORES && pd) {
-                    if (s == 1) put_one(pd->a0, pd->x0);
-                    if (s == KMAX - 2) put_one(pd->a1, pd->x1);
-                }
-            };
+            auto emit = [&](int s, uint32_t h) { pos[s] = POW2 && kRingBfe ? h : ring_pos<POW2>(h, tm); };
             murmur_seeds16<KMAX>(w, k, emit);
         } else if (tid < kps && i < k1) {
             auto emit = [&](int s, uint32_t h) { pos[s] = POW2 && kRingBfe ? h : ring_pos<POW2>(h, tm); };
@@ -327,7 +257,7 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
 #pragma unroll
         for (int u = 0; u < P; ++u) cw[u] = kw[u];
     }
-    hash_sub(k0, cw[0], nullptr);
+    hash_sub(k0, cw[0]);
     // Nothing in flight at the loop's entry: otherwise the wait the compiler places at the loop
     // header, merging the entry path (the first batch's second key load pending) with the back
     // edge, is a full vmcnt(0) that drains every batch's flush stores
@@ -344,7 +274,7 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
             const uint64_t i = s0 + tid;
             const bool live = tid < kps && i < k1;
             lds_barrier();  // previous flush done: ht stable, rings free
-            if (!PBF_DIAG_NOAPPEND && live) {
+            if (live) {
                 uint32_t v[KMAX];
 #pragma unroll
                 for (int s = 0; s < KMAX; ++s)
@@ -392,17 +322,16 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
             }
             // the next sub-chunk's hash (the next batch's keys, at a batch's end), then this
             // flush's stores
-            constexpr bool spread = PBF_SPREAD_STORES && F16 && KMAX >= 3;
             if constexpr (u + 1 < P) {
-                hash_sub(s0 + kps, cw[F16 ? u + 1 : 0], spread ? &pd : nullptr);
+                hash_sub(s0 + kps, cw[F16 ? u + 1 : 0]);
             } else {
                 if constexpr (F16) {
 #pragma unroll
                     for (int x = 0; x < P; ++x) cw[x] = kw[x];
                 }
-                hash_sub(c0 + uint64_t(P) * kps, cw[0], spread ? &pd : nullptr);
+                hash_sub(c0 + uint64_t(P) * kps, cw[0]);
             }
-            if constexpr (!spread) put_groups(pd);
+            put_groups(pd);
             ++j;
         };
         static_assert(P == 2, "two sub-chunks per batch");
@@ -416,7 +345,6 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
         const uint32_t t4 = owner ? ht[tid] & 0xFFFFu : 0u;
         write_groups(t4 > h4, h4);
     }
-    if (PBF_DIAG_SINK && (diag_x.x ^ diag_x.y ^ diag_x.z ^ diag_x.w) == 0x12345678u) fill[0] = 0;
     if (owner) {
         const uint32_t t4 = ht[tid] & 0xFFFFu;
         // fill counts; the probe's remaining cumulative counts
@@ -551,7 +479,7 @@ __device__ __forceinline__ void gather_ring_body(TileMap tm, PartGeom pg, uint64
                 }
 #pragma unroll
                 for (int u = 0; u < U; ++u)
-                    if (anyq[u]) v[u] = PBF_DIAG_GNOLOAD ? make_uint4(lane, r0, u, b0) : ld_stream(entries_at(b0 + u * nwaves, r0 + lane * 4));
+                    if (anyq[u]) v[u] = ld_stream(entries_at(b0 + u * nwaves, r0 + lane * 4));
             } else {
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
@@ -611,10 +539,7 @@ __device__ __forceinline__ void gather_ring_body(TileMap tm, PartGeom pg, uint64
                                 } else {
 #pragma unroll
                                     for (int f = 0; f < NFM; ++f)
-                                        if ((fl[f] >> (8 * t)) & 1u) {
-                                            if (PBF_DIAG_GNOATOM) kbits[(f * kw + (key >> 5)) & 7] = key;  // diagnostic
-                                            else atomicAnd(kbits + f * kw + (key >> 5), ~(1u << (key & 31)));
-                                        }
+                                        if ((fl[f] >> (8 * t)) & 1u) atomicAnd(kbits + f * kw + (key >> 5), ~(1u << (key & 31)));
                                 }
                             }
                         } else {
