@@ -592,7 +592,6 @@ int run_atomic(pbf_filter_t* f, const Batch& b) {
 struct PartPlan {
     PartGeom pg;
     bool pk3;           // counting-sort build with packed entries (k_part / k_tile_build PK3)
-    bool w4;            // counting-sort probe with runs padded to 4 entries, 16-byte write-out (k_part W4)
     size_t lds_part;
     size_t lds_gather;  // probes: per gather workgroup
     uint32_t gsplit;    // probes: gather splits over tile ranges (grid G x gsplit)
@@ -689,15 +688,6 @@ int part_kmax(uint32_t k, int km) {
     return kmax_for(k);
 }
 
-// Probe runs padded to 4 entries with a 16-byte write-out (PBF_W4=0 disables it: A/B).
-bool w4_enabled() {
-    static const bool v = [] {
-        const char* e = std::getenv("PBF_W4");
-        return !(e && e[0] == '0');
-    }();
-    return v;
-}
-
 // Packed build entries (PBF_PK3=0 disables them, for A/B measurements).
 bool pk3_enabled() {
     static const bool v = [] {
@@ -710,26 +700,22 @@ bool pk3_enabled() {
 PartPlan plan_partition(uint32_t B, uint32_t k, int km, uint64_t n, bool probe, double share, uint32_t nf) {
     PartPlan pl{};
     const size_t per_entry = probe ? 6 : 4;  // stage u32 (+ u16 tile id for probes)
-    const size_t fixed = size_t(3 * B + 1 + 16) * 4 + 12;  // (+ the stage's 16-byte alignment)
+    const size_t fixed = size_t(3 * B + 1 + 16) * 4;
     const uint64_t smax = (156 * 1024 - fixed) / per_entry;  // stage entries the LDS holds
     // keys per thread per sub-chunk: as many as the registers allow (part_kpt), placed in at most
     // two windows of the stage
     uint64_t kpt = uint64_t(part_kpt(part_kmax(k, km), km, probe));
-    // padded runs: builds with packed entries (<= 2 pad slots per tile and sub-chunk), probes
-    // with the 16-byte write-out (<= 3), both for the exact-k kernels only
-    const bool exact = km != kFixedN && (k == 6 || k == 8 || k == 10);
-    pl.pk3 = !probe && pk3_enabled() && exact;
-    pl.w4 = probe && w4_enabled() && exact;
-    const uint64_t padk = pl.pk3 ? 2 : (pl.w4 ? 3 : 2);
     // (and k_part keeps ranks and slots as 16-bit halves: kps * k + pads < 2^16)
-    while (kpt > 1 && (kpt * kPartThreads * k > 2 * smax || kpt * kPartThreads * k + padk * std::min<uint64_t>(B, kpt * kPartThreads * k) >= 65536)) --kpt;
+    while (kpt > 1 && (kpt * kPartThreads * k > 2 * smax || kpt * kPartThreads * k + 2 * std::min<uint64_t>(B, kpt * kPartThreads * k) >= 65536)) --kpt;
     // probe sub-chunks tile the 4096-key groups of the entry format: 1, 2 or 4 keys per thread
     if (probe) kpt = kpt >= 4 ? 4 : (kpt >= 2 ? 2 : 1);
     const uint64_t kps = kpt * kPartThreads;
-    const uint64_t need = kps * k + (pl.pk3 || pl.w4 ? padk * std::min<uint64_t>(B, kps * k) : 0);
+    // packed build entries (tiled_kernels.hpp PK3) for the exact-k kernels; their runs are padded
+    // (<= 2 pad slots per tile)
+    pl.pk3 = !probe && pk3_enabled() && km != kFixedN && (k == 6 || k == 8 || k == 10);
+    const uint64_t need = kps * k + (pl.pk3 ? 2 * std::min<uint64_t>(B, kps * k) : 0);
     uint64_t scap = std::min(need, smax);
     if (pl.pk3) scap -= scap % 3;  // windows hold whole packed words
-    if (pl.w4) scap -= scap % 4;   // ... whole 4-entry pieces
     pl.pg.scap = uint32_t(scap);
     pl.lds_part = fixed + size_t(scap) * per_entry;
     const uint64_t G0 = std::min<uint64_t>(part_max_groups(probe), std::max<uint64_t>(1, (n + kps - 1) / kps));
@@ -745,10 +731,6 @@ PartPlan plan_partition(uint32_t B, uint32_t k, int km, uint64_t n, bool probe, 
     // (k_part addresses an entry by a 24-bit multiply-add within its workgroup's regions)
     pl.pg.cap = uint32_t(std::min<uint64_t>(((cap + 31) / 32) * 32, ((uint64_t(1) << 32) - 1) / std::max<uint32_t>(B, 1) & ~uint64_t(31)));
     pl.pg.cap = std::min<uint32_t>(pl.pg.cap, (1u << 24) - 32);
-    if (pl.w4) {  // + the pads (<= 3 per sub-chunk)
-        const uint64_t c4 = uint64_t(pl.pg.cap) + 3 * pl.pg.nsub;
-        pl.pg.cap = uint32_t(std::min<uint64_t>(((c4 + 31) / 32) * 32, (1u << 24) - 32));
-    }
     if (pl.pk3) {
         // + the pads (<= 2 per sub-chunk), in whole 32-word units of 3 entries
         const uint64_t c3 = uint64_t(pl.pg.cap) + 2 * pl.pg.nsub;
@@ -815,18 +797,7 @@ void with_ring_kernel(uint32_t k, bool pow2, L&& launch) {
 // The counting-sort partition kernel for (k, key layout): exact-k variants for the k the
 // configurations use (6: C2/C5 shapes, 8: C3, 10: the fp = 0.001 product sizing of C4 / SSTables).
 template <int KX, int KMD, bool PROBE, class L>
-void with_part_kernel(uint32_t k, L&& launch, bool pk3 = false, bool w4 = false) {
-    if constexpr (KMD != kFixedN && PROBE) {
-        if (w4) {
-            if constexpr (KX == 8) {
-                if (k == 6) return launch(k_part<6, KMD, PROBE, true, false, true>);
-                if (k == 8) return launch(k_part<8, KMD, PROBE, true, false, true>);
-            }
-            if constexpr (KX == 16) {
-                if (k == 10) return launch(k_part<10, KMD, PROBE, true, false, true>);
-            }
-        }
-    }
+void with_part_kernel(uint32_t k, L&& launch, bool pk3 = false) {
     if constexpr (KMD != kFixedN) {
         if constexpr (KX == 8) {
             if constexpr (!PROBE) {
@@ -991,7 +962,7 @@ int run_tiled_probe_set(pbf_filter_t* f, pbf_filter_t* const* fs, uint32_t nf, c
                     if (err == hipSuccess)
                         kern<<<pg.G, kPartThreads, pl.lds_part, s>>>(pks, b.n, int(k), tm, pg, regions, fill, pref,
                                                              nullptr, nullptr, ps, use_hw ? hw : nullptr);
-                }, false, pl.w4);
+                });
             }
         }
     });

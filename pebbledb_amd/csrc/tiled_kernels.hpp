@@ -233,12 +233,8 @@ __host__ __device__ constexpr int part_kpt(int kmax, int km, bool probe) {
 constexpr uint32_t kPk3Bits = 21;
 __device__ __forceinline__ uint32_t div3(uint32_t x) { return __umulhi(x, 0xAAAAAAABu) >> 1; }
 
-// W4 (probes): each tile's run of a sub-chunk is padded to a multiple of 4 entries with copies of
-// its first entry (a copy is tested again and clears the same key: harmless), so the write-out
-// moves 16 B (4 entries) per lane with 16-byte stores instead of one 4-byte entry per lane.
-//
 // EXACT: k == KMAX at compile time (no per-seed branches; the seeds' LDS atomics issue together).
-template <int KMAX, int KM, bool PROBE, bool EXACT = false, bool PK3 = false, bool W4 = false>
+template <int KMAX, int KM, bool PROBE, bool EXACT = false, bool PK3 = false>
 __global__ void __launch_bounds__(kPartThreads) k_part(KeySet ks, uint64_t n, int k, TileMap tm, PartGeom pg,
                                                        uint32_t* __restrict__ regions, uint32_t* __restrict__ fill,
                                                        uint16_t* __restrict__ pref, uint32_t* __restrict__ ovf,
@@ -257,8 +253,7 @@ __global__ void __launch_bounds__(kPartThreads) k_part(KeySet ks, uint64_t n, in
     uint32_t* cnt = cb + B;            // B: the next sub-chunk's per-tile count
     uint32_t* lbase = cnt + B;         // B+1: the current sub-chunk's exclusive scan of its counts
     uint32_t* ws = lbase + B + 1;      // 16
-    // scap (16-byte aligned: W4 reads 4 entries at once; the host allows 12 bytes for it)
-    uint32_t* stage = ws + 16 + ((4u - ((3u * B + 17u) & 3u)) & 3u);
+    uint32_t* stage = ws + 16;         // scap
     uint16_t* bkt = reinterpret_cast<uint16_t*>(stage + pg.scap);  // scap (probes)
     const uint32_t lmask = (1u << tm.tb) - 1u;
     uint32_t* const rgn = regions + uint64_t(g) * B * pg.cap;  // this workgroup's regions
@@ -342,7 +337,7 @@ __global__ void __launch_bounds__(kPartThreads) k_part(KeySet ks, uint64_t n, in
     // + its count - lbase[b]); a previous sub-chunk that closed a 4096-key group leaves the
     // routed count cb[b] + lbase_prev[b + 1] in pref.  A thread scans <= 4 tiles (B <= 4096).
     // Ends synced.
-    auto padded = [](uint32_t c) { return PK3 ? c + (3u - c % 3u) % 3u : (W4 ? (c + 3u) & ~3u : c); };
+    auto padded = [](uint32_t c) { return PK3 ? c + (3u - c % 3u) % 3u : c; };
     auto scan_advance = [&](bool group_end, uint32_t q) {
         const uint32_t per = (B + nt - 1) / nt;
         const uint32_t lo = min(B, tid * per), hi = min(B, lo + per);
@@ -447,11 +442,6 @@ __global__ void __launch_bounds__(kPartThreads) k_part(KeySet ks, uint64_t n, in
                     const uint32_t c = cnt[b], l0 = lbase[b];
                     for (uint32_t y = c; y < padded(c); ++y)
                         if (l0 + y - e_lo < S) stage[l0 + y - e_lo] = (b ^ 1u) << tm.tb;
-                } else if constexpr (W4 && PROBE) {
-                    // the run's 0-3 pad slots, marked (the write-out copies the run's first entry in)
-                    const uint32_t c = cnt[b], l0 = lbase[b];
-                    for (uint32_t y = c; y < padded(c); ++y)
-                        if (l0 + y - e_lo < S) bkt[l0 + y - e_lo] = 0xFFFFu;
                 }
                 if (last) cnt[b] = 0;
             }
@@ -506,44 +496,6 @@ __global__ void __launch_bounds__(kPartThreads) k_part(KeySet ks, uint64_t n, in
                                 ovf[x] = v0[u];
                                 ovf[x + 1] = (v1[u] >> tm.tb) == b[u] ? v1[u] : v0[u];
                                 ovf[x + 2] = (v2[u] >> tm.tb) == b[u] ? v2[u] : v0[u];
-                            }
-                        }
-                    }
-                }
-            } else if constexpr (W4 && PROBE) {
-                // one 4-entry piece of one run per thread and batch slot: 16-byte stage read, tile
-                // and pad marks from the u16 tile ids, 16-byte region store
-                const uint32_t np = nw / 4;  // (tot, e_lo and the stage are multiples of 4)
-                for (uint32_t c0 = tid; c0 < np; c0 += nt * UW) {
-                    uint4 v[UW];
-                    uint32_t b[UW], r[UW];
-#pragma unroll
-                    for (int u = 0; u < UW; ++u) {
-                        const uint32_t c = min(c0 + u * nt, np - 1);
-                        v[u] = *reinterpret_cast<const uint4*>(stage + 4 * c);
-                        const uint2 bb = *reinterpret_cast<const uint2*>(bkt + 4 * c);
-                        b[u] = bb.x & 0xFFFFu;
-                        if ((bb.x >> 16) == 0xFFFFu) v[u].y = v[u].x;
-                        if ((bb.y & 0xFFFFu) == 0xFFFFu) v[u].z = v[u].x;
-                        if ((bb.y >> 16) == 0xFFFFu) v[u].w = v[u].x;
-                    }
-#pragma unroll
-                    for (int u = 0; u < UW; ++u) r[u] = cb[b[u]] + e_lo + 4 * (c0 + u * nt);
-                    uint32_t over = 0;
-#pragma unroll
-                    for (int u = 0; u < UW; ++u) {
-                        const bool live = c0 + u * nt < np;
-                        if (live && r[u] < pg.cap) *reinterpret_cast<uint4*>(rgn + __umul24(b[u], pg.cap) + r[u]) = v[u];
-                        over |= uint32_t(live && r[u] >= pg.cap) << u;
-                    }
-                    if (over) {  // region overflow (pieces never straddle cap: both are multiples of 4)
-#pragma unroll
-                        for (int u = 0; u < UW; ++u) {
-                            if ((over >> u) & 1u) {
-                                const uint32_t vv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-                                for (int q = 0; q < 4; ++q)
-                                    spill_probe(ps, pos_to_bit((b[u] << tm.tb) | (vv[q] & lmask), tm),
-                                                s0 + ((vv[q] >> kSlotShift) & (pg.kps - 1)));
                             }
                         }
                     }
