@@ -931,11 +931,15 @@ int run_tiled_probe_set(pbf_filter_t* f, pbf_filter_t* const* fs, uint32_t nf, c
     ps.neg_stride = neg_words;
     for (uint32_t i = 0; i < nf; ++i) ps.bm[i] = fs[i]->bitmap;
     size_t lds_tile = ((size_t(1) << tm.tb) / 32 + 2 * pg.G + 1 + 16) * 4;
-    // the tile test's per-word table: u32 global word index + u8 filled-entry count per word
-    // (TAB 2, else the u16 region of every word: TAB 1, else a binary search: TAB 0)
-    const size_t table_words = size_t(pg.G) * (pg.cap / 32);
-    const int tab = lds_tile + table_words * 5 <= 160 * 1024 ? 2 : (lds_tile + table_words * 2 <= 160 * 1024 ? 1 : 0);
-    lds_tile += tab == 2 ? table_words * 5 : (tab == 1 ? table_words * 2 : 0);
+    // the tile test's per-word table: the u32 global word index per word (TAB 2), else a u16 of
+    // region << wsh | word-in-region (TAB 1: when both fit 16 bits and region * B + tile 24
+    // bits), else a binary search (TAB 0)
+    const uint32_t wpr = pg.cap / 32;
+    const size_t table_words = size_t(pg.G) * wpr;
+    const uint32_t wsh = 32u - uint32_t(__builtin_clz(std::max(wpr, 2u) - 1u));
+    const bool tab1_fits = (uint64_t(pg.G - 1) << wsh) < 65536 && uint64_t(pg.G) * B < (uint64_t(1) << 24);
+    const int tab = lds_tile + table_words * 4 <= 160 * 1024 ? 2 : (tab1_fits && lds_tile + table_words * 2 <= 160 * 1024 ? 1 : 0);
+    lds_tile += tab == 2 ? table_words * 4 : (tab == 1 ? table_words * 2 : 0);
     // a region word's global index (region * cap/32 + word) is 32-bit
     if (uint64_t(pg.G) * B * (pg.cap / 32) >= (uint64_t(1) << 32)) return fail(PBF_ERR_INVALID, "probe scratch too large");
     auto tprobe = tab == 2 ? k_tile_probe<2> : (tab == 1 ? k_tile_probe<1> : k_tile_probe<0>);

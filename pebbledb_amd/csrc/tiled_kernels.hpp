@@ -703,44 +703,45 @@ __global__ void __launch_bounds__(256) k_ovf_build(TileMap tm, const uint32_t* _
 
 // ------------------------------------------------------------------ probe: tiles
 // Result bits R: one 32-bit word per 32-entry word of a region, bit (8t + l) = entry 4l + t
-// (l = the entry's 16-byte piece of the word, t = its place in the piece).  This is the layout
-// four wave ballots produce when 8 lanes read a word piece by piece (k_tile_probe).
+// (l = the entry's 16-byte piece of the word, t = its place in the piece): lane l of a word's
+// 8 lanes holds entries 4l..4l+3, so the word's result is the OR of the lanes' bits t << (8t + l).
 // One workgroup per tile.  Region words are read 8 per wave instruction: lane = one 16-byte
 // piece of a word, so an instruction reads 1 KiB contiguously (words are consecutive within a
 // region).  Each lane tests its 4 entries in the LDS tile; four ballots give every word's 32
 // result bits, stored by the word's first lane.
 // TAB = 2 (the LDS budget allows it): a per-word table gives word c's global index
 // wo = region * (cap / 32) + word-in-region — the region word's address / 32 AND its result
-// word's index — and its count of filled entries, so a load needs one LDS read and the wave's
-// U loads issue back to back.  TAB = 1 (5 B per word do not fit, 2 B do: C3's 4096 tiles with
-// ~1000-entry regions): a u16 table gives the word's region, its word-in-region and fill come
-// from the region's word prefix and fill (three LDS reads).  TAB = 0: the word's region comes from
-// a binary search over the word prefix.
+// word's index — so a load needs one LDS read and the wave's U loads issue back to back.  TAB = 1
+// (4 B per word do not fit, 2 B do: C3's 4096 tiles, C5's 33M-key pipelines): a u16 per word
+// holds its region and word-in-region (region << wsh | word), again one LDS read, the index then
+// two 24-bit multiply-adds.  TAB = 0: the word's region comes from a binary search over the word
+// prefix.  The test does not mask the entries past a region's fill in its last word: the gather
+// reads only the filled ones (ring_kernels.hpp), and a stale entry's tile word is in the tile.
+// A lane's 4 result bits go to bits 8t + l of the word's result in registers (no ballots): the
+// word's 8 lanes OR their pieces with three DPP moves and its first lane stores it.
 template <bool NT, int TAB>
 __device__ __forceinline__ void tile_probe_body(uint32_t* smem, uint32_t b, const TileMap& tm, const PartGeom& pg,
                                                 const uint32_t* __restrict__ regions, const uint32_t* __restrict__ fill,
                                                 const uint32_t* __restrict__ bitmap, uint32_t* __restrict__ R) {
     const uint32_t B = tm.nbuckets, G = pg.G, cap = pg.cap, wpr = cap / 32;
+    const uint32_t wsh = 32u - __builtin_clz(max(wpr, 2u) - 1u);  // TAB 1: bits of a word-in-region
     const uint32_t W = 1u << (tm.tb - 5);
     uint32_t* tile = smem;          // W
     uint32_t* fills = tile + W;     // G
     uint32_t* wpre = fills + G;     // G+1
     uint32_t* ws = wpre + G + 1;    // 16
-    uint32_t* wo = ws + 16;                                     // G*wpr (TAB 2)
-    uint8_t* wn = reinterpret_cast<uint8_t*>(wo + G * wpr);     // G*wpr (TAB 2)
-    uint16_t* wq = reinterpret_cast<uint16_t*>(ws + 16);        // G*wpr (TAB 1)
+    uint32_t* wo = ws + 16;                               // G*wpr (TAB 2)
+    uint16_t* wq = reinterpret_cast<uint16_t*>(ws + 16);  // G*wpr (TAB 1)
     const uint64_t w0 = tile_word0(b, tm);
     const uint32_t nw = uint32_t(min<uint64_t>(W, tm.total_words - w0));
     const uint32_t tid = threadIdx.x, nt = blockDim.x;
     // The region fills are loaded (and waited for) first; then the bitmap tile goes global -> LDS by
     // LDS-DMA while the word scan and the per-word table are built (no global load in between,
-    // which would wait for the DMA too), and the stream starts once the DMA has landed.  (G <=
-    // blockDim.x: thread q keeps region q's fill in a register.)
-    const bool dma = PBF_TILE_DMA && (w0 & 3) == 0 && nw == W && G <= nt;
-    uint32_t fq_own = 0;
+    // which would wait for the DMA too), and the stream starts once the DMA has landed.
+    const bool dma = PBF_TILE_DMA && (w0 & 3) == 0 && nw == W;
     if (dma) {
-        if (tid < G) fq_own = fill[uint64_t(b) * G + tid];
-        if (tid < G) fills[tid] = (fq_own + 31) >> 5;  // words (waits for the fill load only)
+        for (uint32_t q = tid; q < G; q += nt) fills[q] = (fill[uint64_t(b) * G + q] + 31) >> 5;  // words
+        // (waits for the fill loads only)
         const uint32_t lane = tid & 63, wave = tid >> 6, nwaves = nt >> 6;
         for (uint32_t c = wave; c < W / 256; c += nwaves)  // 1 KiB per wave instruction
             __builtin_amdgcn_global_load_lds(
@@ -752,18 +753,15 @@ __device__ __forceinline__ void tile_probe_body(uint32_t* smem, uint32_t b, cons
     }
     lds_barrier();
     block_exclusive_scan(fills, wpre, G, ws);
-    for (uint32_t q = tid; q < G; q += nt) {
-        const uint32_t fq = dma ? fq_own : fill[uint64_t(b) * G + q];
-        fills[q] = fq;  // entries again
-        if constexpr (TAB == 2) {
+    if constexpr (TAB > 0) {
+        for (uint32_t q = tid; q < G; q += nt) {
             const uint32_t base = uint32_t(region_id(q, b, G, B)) * wpr;
             for (uint32_t c = wpre[q]; c < wpre[q + 1]; ++c) {
-                const uint32_t word = c - wpre[q];
-                wo[c] = base + word;
-                wn[c] = uint8_t(min(fq - word * 32, 32u));
+                if constexpr (TAB == 2)
+                    wo[c] = base + (c - wpre[q]);
+                else
+                    wq[c] = uint16_t((q << wsh) | (c - wpre[q]));
             }
-        } else if constexpr (TAB == 1) {
-            for (uint32_t c = wpre[q]; c < wpre[q + 1]; ++c) wq[c] = uint16_t(q);
         }
     }
     if (dma) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's tile pieces landed
@@ -775,19 +773,18 @@ __device__ __forceinline__ void tile_probe_body(uint32_t* smem, uint32_t b, cons
     constexpr int U = kTileProbeWordsInFlight;  // instructions (8 words each) in flight per wave
     for (uint32_t c0 = wave * 8; c0 < total; c0 += stride * U) {
         uint4 v[U];
-        uint32_t oo[U], lim[U];
+        uint32_t oo[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const uint32_t c = c0 + u * stride + wsub;
-            const uint32_t cc = min(c, total - 1);  // unconditional loads
+            const uint32_t cc = min(c0 + u * stride + wsub, total - 1);  // unconditional loads
             if constexpr (TAB == 2) {
                 oo[u] = wo[cc];
-                lim[u] = c < total ? uint32_t(wn[cc]) : 0u;  // entries past the fill read as 0
+            } else if constexpr (TAB == 1) {
+                const uint32_t e = wq[cc];
+                oo[u] = __umul24(__umul24(e >> wsh, B) + b, wpr) + (e & ((1u << wsh) - 1u));
             } else {
-                const uint32_t qq = TAB == 1 ? uint32_t(wq[cc]) : bucket_of(wpre, G, cc);
-                const uint32_t word = cc - wpre[qq];
-                oo[u] = uint32_t(region_id(qq, b, G, B)) * wpr + word;
-                lim[u] = c < total ? min(fills[qq] - word * 32, 32u) : 0u;
+                const uint32_t qq = bucket_of(wpre, G, cc);
+                oo[u] = uint32_t(region_id(qq, b, G, B)) * wpr + (cc - wpre[qq]);
             }
         }
 #pragma unroll
@@ -798,19 +795,12 @@ __device__ __forceinline__ void tile_probe_body(uint32_t* smem, uint32_t b, cons
         auto bit = [&](uint32_t x) { return __builtin_amdgcn_ubfe(tile[__builtin_amdgcn_ubfe(x, 5u, wbits)], x, 1u); };
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const uint32_t e = l * 4;
-            // one ballot per compare, ANDed as lane masks (a ballot of a combined condition goes
-            // through a VGPR select and a second compare)
-            auto bal = [](bool c) { return __builtin_amdgcn_ballot_w64(c); };
-            const uint64_t m0 = bal(bit(v[u].x) != 0u) & bal(e < lim[u]);
-            const uint64_t m1 = bal(bit(v[u].y) != 0u) & bal(e + 1 < lim[u]);
-            const uint64_t m2 = bal(bit(v[u].z) != 0u) & bal(e + 2 < lim[u]);
-            const uint64_t m3 = bal(bit(v[u].w) != 0u) & bal(e + 3 < lim[u]);
-            if (l == 0 && c0 + u * stride + wsub < total) {
-                const uint32_t sh = wsub * 8;
-                R[oo[u]] = uint32_t((m0 >> sh) & 0xFF) | (uint32_t((m1 >> sh) & 0xFF) << 8) |
-                           (uint32_t((m2 >> sh) & 0xFF) << 16) | (uint32_t((m3 >> sh) & 0xFF) << 24);
-            }
+            uint32_t r = (bit(v[u].x) | (bit(v[u].y) << 8) | (bit(v[u].z) << 16) | (bit(v[u].w) << 24)) << l;
+            // OR over the word's 8 lanes: swap neighbours, pairs, then the two quads
+            r |= uint32_t(__builtin_amdgcn_mov_dpp(int(r), 0xB1, 0xF, 0xF, false));   // quad_perm [1,0,3,2]
+            r |= uint32_t(__builtin_amdgcn_mov_dpp(int(r), 0x4E, 0xF, 0xF, false));   // quad_perm [2,3,0,1]
+            r |= uint32_t(__builtin_amdgcn_mov_dpp(int(r), 0x141, 0xF, 0xF, false));  // row_half_mirror
+            if (l == 0 && c0 + u * stride + wsub < total) R[oo[u]] = r;
         }
     }
 }
