@@ -55,7 +55,10 @@ constexpr bool kNtTileLoad = false;   // bitmap loads into the LDS tiles
 // Regions of loads in flight per wave: the tile build 4, the tile test 8 words, the gather 4
 // (16 loads per wave in the tile test and 8 regions in the gather measured slower).
 constexpr int kTileBuildRegionsInFlight = 4;
-constexpr int kTileProbeWordsInFlight = 8;
+#ifndef PBF_TILE_PROBE_WORDS
+#define PBF_TILE_PROBE_WORDS 8
+#endif
+constexpr int kTileProbeWordsInFlight = PBF_TILE_PROBE_WORDS;
 constexpr int kGatherRegionsInFlight = 4;
 typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
 
