@@ -299,6 +299,35 @@ def test_hitmask_tails(oracle):
         assert bf.may_contain_many(q).all()
 
 
+def test_stale_region_entries_after_a_larger_probe(oracle):
+    """The tile test does not mask a region's last word past its fill (the gather reads only the
+    filled entries): a small probe after a larger one on the same scratch — its regions' tails
+    hold the larger batch's entries — must still equal the oracle, for one filter and for a
+    shared-pipeline set of three (k_tile_probe_set), at an odd key count (partial hit-mask
+    words, the hw -> mask conversion)."""
+    from pebbledb_amd import may_contain_multi
+    nb, k = 2 ** 24, 6  # 128 tiles of 2^20 bits
+    members = [PackedKeys.fixed(splitmix_hex_keys(0x57A1E + f, 0, 400_000)) for f in range(3)]
+    wants = [oracle.build(nb, k, m, omp=True) for m in members]
+    fs = []
+    for m in members:
+        bf = BloomFilter(nb, k)
+        bf.set_build_mode(PBF_BUILD_TILED)
+        bf.add_many(m)
+        bf.set_probe_mode(PBF_PROBE_TILED)
+        fs.append(bf)
+    big = PackedKeys.fixed(np.concatenate([splitmix_hex_keys(0x57A1E, 0, 1_500_000),
+                                           splitmix_hex_keys(0x99, 0, 1_500_000)]))
+    small = PackedKeys.fixed(np.concatenate([splitmix_hex_keys(0x57A1E, 7, 150_000),
+                                             splitmix_hex_keys(0x98, 0, 150_001)]))
+    for q in (big, small, big, small):
+        assert np.array_equal(fs[0].may_contain_many(q, packed=True), oracle.probe(wants[0], k, q, omp=True))
+        assert fs[0].last_probe_mode == PBF_PROBE_TILED
+        got = may_contain_multi(fs, q)
+        for i in range(3):
+            assert np.array_equal(got[i], oracle.probe(wants[i], k, q, omp=True)), (q.n, i)
+
+
 def test_small_host_stage_chunks(oracle, monkeypatch):
     """The host→device chunking path (PBF_STAGE_BYTES) in a child process."""
     import subprocess, sys, os, textwrap
