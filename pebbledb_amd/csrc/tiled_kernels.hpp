@@ -59,6 +59,9 @@ constexpr int kTileBuildRegionsInFlight = 4;
 #define PBF_TILE_PROBE_WORDS 8
 #endif
 constexpr int kTileProbeWordsInFlight = PBF_TILE_PROBE_WORDS;
+// The set tile test (k_tile_probe_set: region lines from L2, TAB 1) keeps 12 in flight: C5 6.62
+// vs 7.01 ms, while the one-filter test is slower with 12 (profiles/r05/ab/tile_words/)
+constexpr int kTileProbeSetWordsInFlight = 12;
 constexpr int kGatherRegionsInFlight = 4;
 typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
 
@@ -710,8 +713,7 @@ __global__ void __launch_bounds__(256) k_ovf_build(TileMap tm, const uint32_t* _
 // 8 lanes holds entries 4l..4l+3, so the word's result is the OR of the lanes' bits t << (8t + l).
 // One workgroup per tile.  Region words are read 8 per wave instruction: lane = one 16-byte
 // piece of a word, so an instruction reads 1 KiB contiguously (words are consecutive within a
-// region).  Each lane tests its 4 entries in the LDS tile; four ballots give every word's 32
-// result bits, stored by the word's first lane.
+// region), U instructions in flight per wave.  Each lane tests its 4 entries in the LDS tile.
 // TAB = 2 (the LDS budget allows it): a per-word table gives word c's global index
 // wo = region * (cap / 32) + word-in-region — the region word's address / 32 AND its result
 // word's index — so a load needs one LDS read and the wave's U loads issue back to back.  TAB = 1
@@ -722,7 +724,7 @@ __global__ void __launch_bounds__(256) k_ovf_build(TileMap tm, const uint32_t* _
 // reads only the filled ones (ring_kernels.hpp), and a stale entry's tile word is in the tile.
 // A lane's 4 result bits go to bits 8t + l of the word's result in registers (no ballots): the
 // word's 8 lanes OR their pieces with three DPP moves and its first lane stores it.
-template <bool NT, int TAB>
+template <bool NT, int TAB, int U = kTileProbeWordsInFlight>
 __device__ __forceinline__ void tile_probe_body(uint32_t* smem, uint32_t b, const TileMap& tm, const PartGeom& pg,
                                                 const uint32_t* __restrict__ regions, const uint32_t* __restrict__ fill,
                                                 const uint32_t* __restrict__ bitmap, uint32_t* __restrict__ R) {
@@ -773,7 +775,6 @@ __device__ __forceinline__ void tile_probe_body(uint32_t* smem, uint32_t b, cons
     const uint32_t lane = tid & 63, wave = tid >> 6, nwaves = nt >> 6;
     const uint32_t l = lane & 7, wsub = lane >> 3;  // piece of the word, word of the instruction
     const uint32_t stride = nwaves * 8;
-    constexpr int U = kTileProbeWordsInFlight;  // instructions (8 words each) in flight per wave
     for (uint32_t c0 = wave * 8; c0 < total; c0 += stride * U) {
         uint4 v[U];
         uint32_t oo[U];
@@ -832,7 +833,7 @@ __global__ void __launch_bounds__(1024) k_tile_probe_set(TileMap tm, PartGeom pg
     const uint32_t b = (t / nf) * 8 + (x & 7);
     if (b >= tm.nbuckets) return;
     // the set's other workgroups of tile b read the same lines: temporal loads keep them in L2
-    tile_probe_body<false, TAB>(smem, b, tm, pg, regions, fill, ps.bm[f], R + f * r_stride);
+    tile_probe_body<false, TAB, kTileProbeSetWordsInFlight>(smem, b, tm, pg, regions, fill, ps.bm[f], R + f * r_stride);
 }
 
 // hw (ANDed gather words, one per 32 keys) → the LSB-first hit masks of n keys, for every filter
