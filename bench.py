@@ -83,8 +83,10 @@ def rank_plan(config: str, world: int, rank: int, local: int, c4_keys: int = 125
         1B keys over the 8 filters, shard.key_range).
     c5: 'keys' layout — every rank holds all 8 filters (1 GiB of bitmaps) and probes its 1/world
         slice of the 100M-key batch (whole 64-key hit-mask words) through the fused multi-filter
-        path; 'filters' layout — filters_for_rank(8, world, rank) against the whole batch.  No
-        collective in either: the slices / filters are independent."""
+        path; it builds only filters_for_rank(8, world, rank) (`builds`) and receives the others
+        once by replication (shard.exchange_bitmaps: an all-gather, before timing);
+        'filters' layout — filters_for_rank(8, world, rank) against the whole batch.  No
+        collective on the data path in either: the slices / filters are independent."""
     from pebbledb_amd.shard import filters_for_rank, key_range
     plan = {"rank": rank, "world": world, "device": local}
     if config == "c4":
@@ -95,9 +97,12 @@ def rank_plan(config: str, world: int, rank: int, local: int, c4_keys: int = 125
             words = (c5_probes + 63) // 64
             a = min(c5_probes, (words * rank // world) * 64)
             b = min(c5_probes, (words * (rank + 1) // world) * 64)
-            plan.update(filters=list(range(8)), probe_keys=(a, b), layout="keys")
+            # the rank builds its own share of the filters once; the rest arrive by replication
+            plan.update(filters=list(range(8)), builds=filters_for_rank(8, world, rank), probe_keys=(a, b),
+                        layout="keys")
         else:
-            plan.update(filters=filters_for_rank(8, world, rank), probe_keys=(0, c5_probes), layout="filters")
+            fl = filters_for_rank(8, world, rank)
+            plan.update(filters=fl, builds=fl, probe_keys=(0, c5_probes), layout="filters")
     else:
         plan.update(filters=[rank])
     return plan
@@ -529,13 +534,62 @@ def sets_main(args, rank, world, local, torch, dist, np):
         nq = qb - qa
         filters = {}
         kb = torch.empty(n_f * 16, dtype=torch.uint8, device="cuda")
-        for g in mine:
+
+        def build_filter(g):
             _native.check(L.pbf_gen_splitmix_hex(local, None, kb.data_ptr(), SEED, g * n_f, n_f), "gen")
             torch.cuda.synchronize()
             bf = BloomFilter(nb_bytes, k, device=local)
             bf.add_device_fixed(kb.data_ptr(), 16, n_f)
             bf.sync()
-            filters[g] = bf
+            return bf
+        # Each filter is built ONCE, by its owner (filters_for_rank): in the key-partitioned layout
+        # the other ranks' filters arrive by replication (pebbledb builds a filter per SSTable,
+        # src/sstable.py:274, and every get probes all of them, src/lsm_storage.py:164-179)
+        own = plan["builds"]
+        replicated = own != mine
+        for g in own:
+            filters[g] = build_filter(g)
+        replication = None
+        if replicated and sim:
+            # one GPU: the other ranks' filters are built here as stand-ins (untimed), then copied
+            # into this rank's set with pbf_copy_filter (same device; across GPUs of one process
+            # it is a peer copy over xGMI)
+            stand = {g: build_filter(g) for g in mine if g not in filters}
+            torch.cuda.synchronize()
+            t_r = time.perf_counter()
+            for g, bf in stand.items():
+                filters[g] = bf.replicate(local)
+            replicate_ms = (time.perf_counter() - t_r) * 1e3
+            del stand
+            replication = {"replicate_ms": round(replicate_ms, 3), "filters_received": len(mine) - len(own),
+                           "how": "pbf_copy_filter on this GPU (simulated rank; the real job all-gathers over RCCL)"}
+        elif replicated:
+            from pebbledb_amd.shard import exchange_bitmaps
+            on_dev = dist.get_backend() == "nccl"
+
+            def export(g, t):
+                if on_dev:
+                    filters[g].bitmap_to_device(t.data_ptr())
+                    filters[g].sync()
+                else:
+                    t.copy_(torch.frombuffer(bytearray(filters[g].bitmap()), dtype=torch.uint8))
+
+            def load(g, t):
+                if on_dev:
+                    filters[g] = BloomFilter.from_device_bitmap(t.data_ptr(), nb_bytes, k, device=local,
+                                                                stream=torch.cuda.current_stream().cuda_stream)
+                else:
+                    filters[g] = BloomFilter.from_bytes(t.numpy().tobytes() + bytes([k]), device=local)
+                filters[g].sync()
+            dist.barrier()
+            torch.cuda.synchronize()
+            t_r = time.perf_counter()
+            info = exchange_bitmaps(dist, torch, 8, nb_bytes, export, load, device=local)
+            torch.cuda.synchronize()
+            replicate_ms = (time.perf_counter() - t_r) * 1e3
+            replicate_ms = float(all_reduce_scalar(torch, dist, replicate_ms, dist.ReduceOp.MAX, torch.float64))
+            replication = {"replicate_ms": round(replicate_ms, 3), "filters_received": len(mine) - len(own),
+                           "bytes_received_per_rank": info["bytes_received"], "how": info["collective"]}
         del kb
         q = torch.empty(max(nq, 1) * 16, dtype=torch.uint8, device="cuda")
         half = nq_all // 2
@@ -671,6 +725,10 @@ def sets_main(args, rank, world, local, torch, dist, np):
                                  "fp_within_3x_expected": bool(fp_ok), "probe_detail": hex(s0.last_probe_detail)})
             if host_c5 is not None:
                 out["host_resident"] = host_c5
+            if replication is not None:
+                # one-time: the layout's filters arrive once, then every step probes them
+                replication["built_here"] = own
+                out["replication"] = replication
             if world == 1 and not args.no_cpu_baseline:
                 out["cpu_baseline"] = c5_cpu_baseline(args, filters, mine, hms, q, n_f, nb_bytes, k, np)
                 out["check"]["oracle_sample_equal"] = out["cpu_baseline"].pop("oracle_sample_equal")

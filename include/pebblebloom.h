@@ -182,6 +182,25 @@ int pbf_get_bitmap(pbf_filter_t* f, uint8_t* out, uint64_t nb_bytes);
 /* from_bytes() (bloom_filter.py:83-90): loads an nb_bytes-byte bitmap from host memory. */
 int pbf_set_bitmap(pbf_filter_t* f, const uint8_t* in, uint64_t nb_bytes);
 
+/* from_bytes() / to_bytes() against DEVICE memory on the filter's device (nb_bytes bytes, the
+ * little-endian bitmap without the k byte), e.g. a tensor an RCCL all-gather filled with other
+ * ranks' filters.  Asynchronous on the filter's stream (order a producer on another stream with
+ * pbf_wait_stream, a consumer with pbf_signal_stream or pbf_sync). */
+int pbf_set_bitmap_device(pbf_filter_t* f, const void* in_dev, uint64_t nb_bytes);
+int pbf_get_bitmap_device(pbf_filter_t* f, void* out_dev, uint64_t nb_bytes);
+
+/* A replica of a built filter on dst_device (the same device or another): *out = a new handle
+ * with src's nb_bytes, k and bitmap -- what from_bytes(src.to_bytes()) onto that device gives
+ * (src/sstable.py:99-100), without the host round trip.  The bitmap goes device to device
+ * (hipMemcpyPeerAsync over xGMI, peer access enabled once per device pair where the platform
+ * allows it; the runtime stages the copy otherwise), or with flags = PBF_COPY_BOUNCE through
+ * pinned host memory.  Synchronous: the replica is complete on return and src may change after.
+ * An LSM builds each SSTable's filter once (src/sstable.py:274) and every get probes all of them
+ * (src/lsm_storage.py:164-179): the key-partitioned multi-GPU layout holds every filter on every
+ * GPU by replication, not by rebuilding. */
+#define PBF_COPY_BOUNCE 1
+int pbf_copy_filter(pbf_filter_t* src, int dst_device, int flags, pbf_filter_t** out);
+
 /* Population count of the bitmap (device reduction; host-visible result). */
 int pbf_popcount(pbf_filter_t* f, uint64_t* out);
 
@@ -311,6 +330,10 @@ int pbf_gen_varlen(int device, void* stream, uint8_t* out_dev, const uint64_t* o
 
 /* Message of the last failure on this thread ("" if none). */
 const char* pbf_last_error(void);
+
+/* sha256 (hex) of the kernel sources the library was compiled from (pebbledb_amd/build.py
+ * source_digest()); the Python binding refuses a library whose digest is not the tree's. */
+const char* pbf_source_digest(void);
 
 #ifdef __cplusplus
 }

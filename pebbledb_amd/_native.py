@@ -22,6 +22,7 @@ PBF_PROBE_AUTO, PBF_PROBE_DIRECT, PBF_PROBE_TILED = 0, 1, 2
 PBF_DETAIL_RING, PBF_DETAIL_SORT, PBF_DETAIL_ONE_KEY, PBF_DETAIL_SET, PBF_DETAIL_PACKED = 1, 2, 4, 8, 16
 PBF_DETAIL_SHARED = 32
 PBF_DETAIL_RESIDENT = 64
+PBF_COPY_BOUNCE = 1
 
 _u8p = ctypes.c_void_p
 _vp = ctypes.c_void_p
@@ -53,6 +54,9 @@ SIGNATURES = {
     "pbf_get_bitmap": (_int, [_vp, _u8p, _u64]),
     "pbf_set_bitmap": (_int, [_vp, _u8p, _u64]),
     "pbf_popcount": (_int, [_vp, ctypes.POINTER(_u64)]),
+    "pbf_set_bitmap_device": (_int, [_vp, _vp, _u64]),
+    "pbf_get_bitmap_device": (_int, [_vp, _vp, _u64]),
+    "pbf_copy_filter": (_int, [_vp, _int, _int, ctypes.POINTER(_vp)]),
     "pbf_sync": (_int, [_vp]),
     "pbf_stream": (_vp, [_vp]),
     "pbf_index_params": (_int, [_u64, ctypes.POINTER(_u32), ctypes.POINTER(_u64), ctypes.POINTER(_u32)]),
@@ -79,6 +83,7 @@ SIGNATURES = {
     "pbf_gen_splitmix_hex": (_int, [_int, _vp, _u8p, _u64, _u64, _u64]),
     "pbf_gen_varlen": (_int, [_int, _vp, _u8p, _vp, _u64, _u64, _u64]),
     "pbf_last_error": (ctypes.c_char_p, []),
+    "pbf_source_digest": (ctypes.c_char_p, []),
 }
 
 _lib = None
@@ -108,6 +113,13 @@ def lib():
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
+    # a library compiled from other kernel sources than the tree's is never used (a prebuilt .so
+    # travels to the GPU box with the tree): build() rebuilds it
+    from . import build
+    have, want = L.pbf_source_digest().decode(), build.source_digest()
+    if have != want:
+        raise NativeError(f"{LIB_PATH} is stale: compiled from sources {have[:16]}, the tree's are {want[:16]}; "
+                          "run `python -c 'import __graft_entry__ as g; g.build()'`")
     _lib = L
     return L
 

@@ -11,13 +11,15 @@ The bitmap lives in HBM behind a ``pbf_filter_t`` handle (libpebblebloom.so, cty
 ``add()`` calls are buffered on the host and sent as one batch at the next read (probe,
 serialisation, ``bits``), so an SSTableBuilder-style loop of ``add`` costs one kernel
 pipeline, not one launch per key.  ``may_contain(key)`` — LsmStorage.get's per-key call — is
-one kernel launch that reads the key from mapped pinned memory (``pbf_may_contain``).  Batch
+answered by the device's resident reader wave (the key posted into mapped pinned memory, no
+launch per key; ``pbf_may_contain``), or one launch where the resident reader does not apply.  Batch
 entry points ``add_many`` / ``may_contain_many`` take ``list[str]``, ``PackedKeys`` or a
 ``KeyPacker`` directly.
 
 Thread safety: the reference probes a filter from any reader thread without a lock
-(lsm_storage.py:153-179).  Here every native call takes the handle's mutex, and the host-side
-``add`` buffer has its own lock, so concurrent ``add`` / ``may_contain`` on one filter are safe.
+(lsm_storage.py:153-179).  Here builds, loads and batch probes hold the handle's lock
+exclusively; one-key probes of a built filter hold it shared, so reader threads probe one filter
+concurrently; the host-side ``add`` buffer has its own lock.
 """
 from __future__ import annotations
 
@@ -46,6 +48,22 @@ def _vp(a: np.ndarray | None):
     return None if a is None else ctypes.c_void_p(a.ctypes.data)
 
 
+_FAST = None
+
+
+def _fast():
+    """csrc/fastcall.c (_pebblefast), bound to the loaded library's per-key entry points: the
+    per-key calls go from a str to pbf_may_contain[_set] without ctypes."""
+    global _FAST
+    if _FAST is None:
+        from . import _pebblefast
+        L = _native.lib()
+        _pebblefast.bind(ctypes.cast(L.pbf_may_contain, ctypes.c_void_p).value,
+                         ctypes.cast(L.pbf_may_contain_set, ctypes.c_void_p).value)
+        _FAST = _pebblefast
+    return _FAST
+
+
 class BloomFilter:
     """See module docstring; reference: src/bloom_filter.py:8."""
 
@@ -59,6 +77,7 @@ class BloomFilter:
         self._pending: list[str] = []
         self._plock = threading.Lock()  # guards _pending (add / flush from several threads)
         self._h = None
+        self._hv = 0  # the handle as an int (the per-key fast path)
         # the part of a `bits` int outside the bitmap (bits >= 8*nb_bytes, or a negative int's
         # sign extension): the reference keeps the whole int (bloom_filter.py:31) and compares it
         # in __eq__ (:36), while only the low 8*nb_bytes bits are ever read or serialised
@@ -68,6 +87,7 @@ class BloomFilter:
             _native.check(_native.lib().pbf_create(self.device, nb_bytes, nb_hash_functions, ctypes.byref(h)),
                           "pbf_create")
             self._h = h
+            self._hv = h.value
         if bits:
             self._upload_int(bits)
 
@@ -199,14 +219,19 @@ class BloomFilter:
 
     def may_contain(self, key: str) -> bool:
         """bloom_filter.py:67-74 for one key (pbf_may_contain: answered by the device's resident
-        reader wave, or one launch)."""
-        if self.nb_hash_functions <= 0 or self.nb_bytes <= 0:
-            if not self._require_modulus():
-                return True  # k == 0: the AND over no bits
+        reader wave, or one launch), called from C (_pebblefast) with the str's UTF-8 bytes."""
         if self._pending:
             self._flush()
+        if self._hv and self.nb_hash_functions > 0:
+            r = (_FAST or _fast()).may_contain(self._hv, key)
+            if r is True or r is False:
+                return r
+            if r != -100:  # (-100: not a str; the reference's key.encode raises below)
+                _native.check(r, "pbf_may_contain")
+        enc = key.encode("utf-8")  # first, as bloom_filter.py:43 (AttributeError for a non-str)
+        if not self._require_modulus():
+            return True  # k == 0: the AND over no bits
         out = ctypes.c_int(0)
-        enc = key.encode("utf-8")
         rc = _native.lib().pbf_may_contain(self._h, enc, len(enc), ctypes.byref(out))
         if rc:
             _native.check(rc, "pbf_may_contain")
@@ -228,6 +253,52 @@ class BloomFilter:
             arr = np.frombuffer(data, dtype=np.uint8, count=nb_bytes)
             _native.check(_native.lib().pbf_set_bitmap(bf._h, _vp(arr), nb_bytes), "pbf_set_bitmap")
         return bf
+
+    def replicate(self, device: Optional[int] = None, bounce: bool = False) -> "BloomFilter":
+        """A copy of this filter on `device` (default: this filter's device): what
+        ``from_bytes(self.to_bytes(), device)`` gives, device to device (pbf_copy_filter: peer
+        copy over xGMI, or through pinned host memory with bounce=True).  The key-partitioned
+        multi-GPU probe holds every SSTable's filter on every GPU this way: pebbledb builds a
+        filter once per SSTable (src/sstable.py:274) and every get probes all of them
+        (src/lsm_storage.py:164-179)."""
+        dev = self.device if device is None else int(device)
+        bf = object.__new__(type(self))
+        bf.nb_bytes, bf.bits_size, bf.nb_hash_functions = self.nb_bytes, self.bits_size, self.nb_hash_functions
+        bf.device = dev
+        bf._pending = []
+        bf._plock = threading.Lock()
+        bf._h = None
+        bf._hv = 0
+        bf._extra = self._extra
+        if self.nb_bytes > 0:
+            self._flush()
+            h = ctypes.c_void_p()
+            _native.check(_native.lib().pbf_copy_filter(self._h, dev, _native.PBF_COPY_BOUNCE if bounce else 0,
+                                                        ctypes.byref(h)), "pbf_copy_filter")
+            bf._h = h
+            bf._hv = h.value
+        return bf
+
+    @classmethod
+    def from_device_bitmap(cls, ptr: int, nb_bytes: int, nb_hash_functions: int,
+                           device: Optional[int] = None, stream: int = 0) -> "BloomFilter":
+        """from_bytes() of a bitmap already in device memory on `device` (nb_bytes at `ptr`,
+        e.g. a tensor an all-gather filled): no host copy.  `stream`: the producer's stream (its
+        work is ordered before the load); the load is asynchronous on the filter's stream."""
+        bf = cls(nb_bytes=nb_bytes, nb_hash_functions=nb_hash_functions, device=device)
+        if nb_bytes > 0:
+            bf.wait_stream(stream)
+            _native.check(_native.lib().pbf_set_bitmap_device(bf._h, ctypes.c_void_p(ptr), nb_bytes),
+                          "pbf_set_bitmap_device")
+        return bf
+
+    def bitmap_to_device(self, ptr: int) -> None:
+        """to_bytes() without the k byte into device memory on this filter's device (nb_bytes at
+        `ptr`); asynchronous on the filter's stream (sync() or signal_stream() before reading)."""
+        if self.nb_bytes > 0:
+            self._flush()
+            _native.check(_native.lib().pbf_get_bitmap_device(self._h, ctypes.c_void_p(ptr), self.nb_bytes),
+                          "pbf_get_bitmap_device")
 
     @classmethod
     def build_from_keys_and_fp_rate(cls, keys, fp_rate: float, device: Optional[int] = None) -> "BloomFilter":
@@ -430,17 +501,22 @@ def may_contain_set(filters, key: str) -> list[bool]:
     nf = len(filters)
     if not nf:
         return []
-    enc = key.encode("utf-8")
-    # the common shape (LsmStorage.get: built filters, k > 0, one device): one call, no numpy
+    # the common shape (LsmStorage.get: built filters, k > 0, one device, <= 64 of them): one C
+    # call (_pebblefast), no ctypes or numpy
     dev0 = filters[0].device
-    if all(bf.nb_hash_functions > 0 and bf.nb_bytes > 0 and not bf._pending and bf.device == dev0 for bf in filters):
-        hs = (ctypes.c_void_p * nf)(*[bf._h.value for bf in filters])
-        out = (ctypes.c_uint8 * ((nf + 7) // 8))()
-        rc = _native.lib().pbf_may_contain_set(hs, nf, enc, len(enc), out)
-        if rc:
-            _native.check(rc, "pbf_may_contain_set")
-        bits = int.from_bytes(bytes(out), "little")
-        return [(bits >> j) & 1 == 1 for j in range(nf)]
+    if nf <= 64:
+        hs = []
+        for bf in filters:
+            if bf._pending or bf.nb_hash_functions <= 0 or not bf._hv or bf.device != dev0:
+                break
+            hs.append(bf._hv)
+        else:
+            rc, bits = (_FAST or _fast()).may_contain_set(hs, key)
+            if rc == 0:
+                return [(bits >> j) & 1 == 1 for j in range(nf)]
+            if rc != -100:
+                _native.check(rc, "pbf_may_contain_set")
+    enc = key.encode("utf-8")
     native = _native_set(filters)
     res = [True] * nf  # k == 0: the AND over no bits
     for dev in dict.fromkeys(filters[i].device for i in native):  # one call per device

@@ -52,11 +52,28 @@ def source_digest() -> str:
     return h.hexdigest()
 
 
+DIGEST_MARKER = b"pbf-source-digest:"
+
+
+def embedded_digest(path: str = LIB) -> str | None:
+    """The source_digest() a library was compiled from (build_lib passes it as PBF_SOURCE_DIGEST
+    and the library keeps it behind DIGEST_MARKER), read from the file without loading it; None
+    for a library built without one."""
+    if not os.path.exists(path):
+        return None
+    with open(path, "rb") as fh:
+        data = fh.read()
+    i = data.find(DIGEST_MARKER)
+    if i < 0:
+        return None
+    d = data[i + len(DIGEST_MARKER):i + len(DIGEST_MARKER) + 64]
+    return d.decode("ascii", "replace") if len(d) == 64 else None
+
+
 def up_to_date() -> bool:
-    if not os.path.exists(LIB):
-        return False
-    t = os.path.getmtime(LIB)
-    return all(os.path.getmtime(d) <= t for d in DEPS)
+    """The library exists and was compiled from the sources in the tree (its embedded digest,
+    not file times: a prebuilt .so travels to the GPU box with the tree)."""
+    return embedded_digest(LIB) == source_digest()
 
 
 def build_lib(force: bool = False, verbose: bool = True, out: str = LIB, defines=()) -> str:
@@ -65,7 +82,8 @@ def build_lib(force: bool = False, verbose: bool = True, out: str = LIB, defines
     if not force and out == LIB and not defines and up_to_date():
         return LIB
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-Wall", "-Wno-unused-result"] + [f"-D{d}" for d in defines] + ["-o", out + ".tmp"] + SOURCES
+           "-Wall", "-Wno-unused-result", f'-DPBF_SOURCE_DIGEST="{source_digest()}"'] + \
+        [f"-D{d}" for d in defines] + ["-o", out + ".tmp"] + SOURCES
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
@@ -81,20 +99,37 @@ def ingest_path() -> str:
     return os.path.join(PKG, "_pebbleingest" + sysconfig.get_config_var("EXT_SUFFIX"))
 
 
-def build_ingest(force: bool = False, verbose: bool = True) -> str:
-    """The host-side packed-ingestion extension (csrc/ingest.c, CPython C API, gcc)."""
+def _build_ext(src: str, out: str, force: bool, verbose: bool, openmp: bool) -> str:
     import sysconfig
-    out = ingest_path()
-    if not force and os.path.exists(out) and os.path.getmtime(out) >= os.path.getmtime(INGEST_SRC):
+    if not force and os.path.exists(out) and os.path.getmtime(out) >= os.path.getmtime(src):
         return out
-    cmd = [os.environ.get("CC", "gcc"), "-O2", "-fPIC", "-shared", "-fopenmp", "-Wall", "-Wextra",
-           "-Wno-missing-field-initializers", "-Wno-unused-parameter", "-I", sysconfig.get_paths()["include"],
-           "-o", out + ".tmp", INGEST_SRC]
+    cmd = [os.environ.get("CC", "gcc"), "-O2", "-fPIC", "-shared"] + (["-fopenmp"] if openmp else []) + \
+        ["-Wall", "-Wextra", "-Wno-missing-field-initializers", "-Wno-unused-parameter", "-Wno-cast-function-type",
+         "-I", sysconfig.get_paths()["include"], "-o", out + ".tmp", src]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
     os.replace(out + ".tmp", out)
     return out
+
+
+def build_ingest(force: bool = False, verbose: bool = True) -> str:
+    """The host-side packed-ingestion extension (csrc/ingest.c, CPython C API, gcc)."""
+    return _build_ext(INGEST_SRC, ingest_path(), force, verbose, openmp=True)
+
+
+FAST_SRC = os.path.join(CSRC, "fastcall.c")
+
+
+def fast_path() -> str:
+    import sysconfig
+    return os.path.join(PKG, "_pebblefast" + sysconfig.get_config_var("EXT_SUFFIX"))
+
+
+def build_fast(force: bool = False, verbose: bool = True) -> str:
+    """The per-key call extension (csrc/fastcall.c: may_contain / may_contain_set without
+    ctypes, CPython C API, gcc)."""
+    return _build_ext(FAST_SRC, fast_path(), force, verbose, openmp=False)
 
 
 if __name__ == "__main__":

@@ -1779,6 +1779,7 @@ ResidentReader* resident_reader(int device) {
     if (it != g_resident.end()) return it->second;
     ResidentReader* rr = nullptr;
     do {
+        if (hipSetDevice(device) != hipSuccess) break;  // (the one-key callers do not set it)
         void* h = nullptr;
         if (hipHostMalloc(&h, sizeof(SvcBoard), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) break;
         std::memset(h, 0, sizeof(SvcBoard));
@@ -1913,7 +1914,18 @@ int resident_probe(int device, const SvcFilter* fs, uint32_t nf, uint32_t k, con
                 rc = resident_ensure(rr);
                 if (rc) return rc;
             }
-            if (el > std::chrono::seconds(2)) return fail(PBF_ERR_HIP, "resident reader: no answer within 2 s");
+            if (el > std::chrono::seconds(2)) {
+                // Retract the request before the caller may free or rebuild the bitmap: a wave
+                // that has not taken it yet acknowledges a head with no filters without reading
+                // any memory; one that has taken it answers within microseconds of doing so.
+                __atomic_store_n(&hd.nf, 0u, __ATOMIC_RELEASE);
+                const auto t1 = std::chrono::steady_clock::now();
+                while (__atomic_load_n(&sl.ack, __ATOMIC_ACQUIRE) != seq &&
+                       __atomic_load_n(&rr->host->state, __ATOMIC_ACQUIRE) != 0 &&
+                       std::chrono::steady_clock::now() - t1 < std::chrono::milliseconds(100)) {
+                }
+                return fail(PBF_ERR_HIP, "resident reader: no answer within 2 s (request retracted)");
+            }
         }
     }
     *bits = __atomic_load_n(&sl.bits, __ATOMIC_ACQUIRE);
@@ -1939,23 +1951,26 @@ bool reader_ok(pbf_filter_t* f, uint64_t len) {
     return q == hipSuccess;
 }
 
-// The mapped one-key probe of f on stream s.  shared: the caller holds f's lock shared (reader_ok
-// held), so nothing of the handle is written but the probe diagnostics (atomics).
+// One key of a built filter (reader_ok, lock held shared) through the resident reader:
+// PBF_OK with *out, an error, or kNotTaken when the reader does not take it (the caller launches).
+constexpr int kNotTaken = 1;
+int one_key_resident(pbf_filter_t* f, const uint8_t* key, uint64_t len, int* out) {
+    SvcFilter sf{f->bitmap, f->im};
+    uint64_t bits = 0;
+    bool taken = false;
+    const int rc = resident_probe(f->device, &sf, 1, f->k, key, len, &bits, &taken);
+    if (rc) return rc;
+    if (!taken) return kNotTaken;
+    *out = int(bits & 1u);
+    f->last_probe_mode = PBF_PROBE_DIRECT;
+    f->last_probe_detail = PBF_DETAIL_ONE_KEY | PBF_DETAIL_SHARED | PBF_DETAIL_RESIDENT;
+    return PBF_OK;
+}
+
+// The mapped one-key probe of f on stream s (a launch).  shared: the caller holds f's lock shared
+// (reader_ok held), so nothing of the handle is written but the probe diagnostics (atomics).
 int one_key_probe(pbf_filter_t* f, const uint8_t* key, uint64_t len, int* out, hipStream_t s, bool shared) {
     int rc = PBF_OK;
-    if (shared) {  // no work of f queued (reader_ok): the resident reader may answer
-        SvcFilter sf{f->bitmap, f->im};
-        uint64_t bits = 0;
-        bool taken = false;
-        rc = resident_probe(f->device, &sf, 1, f->k, key, len, &bits, &taken);
-        if (rc) return rc;
-        if (taken) {
-            *out = int(bits & 1u);
-            f->last_probe_mode = PBF_PROBE_DIRECT;
-            f->last_probe_detail = PBF_DETAIL_ONE_KEY | PBF_DETAIL_SHARED | PBF_DETAIL_RESIDENT;
-            return PBF_OK;
-        }
-    }
     OneKeyStage* st = nullptr;
     rc = one_key_stage(f->device, &st);
     if (rc) return rc;
@@ -2167,6 +2182,79 @@ int may_contain_set_locked(pbf_filter_t* const* fs, uint32_t nf, const uint8_t* 
 
 }  // namespace
 
+namespace {
+
+// Peer access from device a to device b's memory, enabled once per pair where the platform allows
+// (xGMI between MI355X GPUs of a node); hipMemcpyPeerAsync stages through the host otherwise.
+void enable_peer(int a, int b) {
+    if (a == b) return;
+    static std::mutex mu;
+    static std::map<std::pair<int, int>, bool> done;
+    std::lock_guard<std::mutex> lock(mu);
+    if (done.count({a, b})) return;
+    int can = 0;
+    if (hipDeviceCanAccessPeer(&can, a, b) == hipSuccess && can && hipSetDevice(a) == hipSuccess) {
+        const hipError_t e = hipDeviceEnablePeerAccess(b, 0);
+        (void)e;  // hipErrorPeerAccessAlreadyEnabled is fine too
+    }
+    (void)hipGetLastError();
+    done[{a, b}] = true;
+}
+
+// dst (just created with src's nb_bytes and k) receives src's bitmap: device to device, or through
+// pinned host memory (bounce).  Synchronous.  src's lock is held by the caller.
+int copy_filter_into(pbf_filter_t* src, pbf_filter_t* dst, bool bounce) {
+    dst->mode = src->mode;
+    dst->probe_mode = src->probe_mode;
+    if (src->pristine) {
+        // logically all zero: the replica as created is that already (its unreachable middle,
+        // m > 2^32, zeroed by pbf_create; a pristine src has a clean middle, pbf_clear)
+        HIP_TRY(hipSetDevice(dst->device));
+        return wait_stream(dst);
+    }
+    HIP_TRY(hipSetDevice(src->device));
+    int rc = wait_stream(src);  // src's last build / load is in its bitmap
+    if (rc) return rc;
+    HIP_TRY(hipSetDevice(dst->device));
+    rc = wait_stream(dst);  // the replica's allocation and zeroing are done
+    if (rc) return rc;
+    const size_t bytes = size_t(src->alloc_words) * 4;  // (the tail past nb_bytes is zero in src)
+    if (!bounce) {
+        if (src->device == dst->device) {
+            HIP_TRY(hipMemcpyAsync(dst->bitmap, src->bitmap, bytes, hipMemcpyDeviceToDevice, dst->stream));
+        } else {
+            enable_peer(dst->device, src->device);
+            HIP_TRY(hipSetDevice(dst->device));
+            HIP_TRY(hipMemcpyPeerAsync(dst->bitmap, dst->device, src->bitmap, src->device, bytes, dst->stream));
+        }
+    } else {
+        // pinned host bounce in 64 MiB pieces, each D2H on src's stream then H2D on dst's
+        const size_t piece = std::min<size_t>(bytes, size_t(64) << 20);
+        void* host = nullptr;
+        HIP_TRY(hipHostMalloc(&host, piece, hipHostMallocDefault));
+        hipError_t e = hipSuccess;
+        for (size_t o = 0; o < bytes && e == hipSuccess; o += piece) {
+            const size_t c = std::min(piece, bytes - o);
+            e = hipSetDevice(src->device);
+            if (e == hipSuccess)
+                e = hipMemcpyAsync(host, reinterpret_cast<uint8_t*>(src->bitmap) + o, c, hipMemcpyDeviceToHost, src->stream);
+            if (e == hipSuccess) e = hipStreamSynchronize(src->stream);
+            if (e == hipSuccess) e = hipSetDevice(dst->device);
+            if (e == hipSuccess)
+                e = hipMemcpyAsync(reinterpret_cast<uint8_t*>(dst->bitmap) + o, host, c, hipMemcpyHostToDevice, dst->stream);
+            if (e == hipSuccess) e = hipStreamSynchronize(dst->stream);
+        }
+        (void)hipHostFree(host);
+        HIP_TRY(e);
+    }
+    dst->pristine = false;
+    dst->middle_dirty = src->middle_dirty;
+    dst->pending = true;
+    return wait_stream(dst);
+}
+
+}  // namespace
+
 extern "C" {
 
 int pbf_version(void) { return 100; }
@@ -2178,6 +2266,13 @@ int pbf_device_count(int* count) {
 }
 
 const char* pbf_last_error(void) { return g_last_error.c_str(); }
+
+#ifndef PBF_SOURCE_DIGEST
+#define PBF_SOURCE_DIGEST "none"
+#endif
+// the digest behind a marker, so build.py reads it from the file without loading the library
+__attribute__((used)) const char pbf_source_digest_tag[] = "pbf-source-digest:" PBF_SOURCE_DIGEST;
+const char* pbf_source_digest(void) { return pbf_source_digest_tag + 18; }
 
 int pbf_create(int device, uint64_t nb_bytes, uint32_t nb_hash_functions, pbf_filter_t** out) {
     if (!out) return fail(PBF_ERR_INVALID, "null out");
@@ -2471,6 +2566,55 @@ int pbf_set_bitmap(pbf_filter_t* f, const uint8_t* in, uint64_t nb_bytes) {
     return PBF_OK;
 }
 
+int pbf_set_bitmap_device(pbf_filter_t* f, const void* in_dev, uint64_t nb_bytes) {
+    LOCK(f);
+    int rc = enter(f);
+    if (rc) return rc;
+    if (nb_bytes != f->nb_bytes) return fail(PBF_ERR_INVALID, "nb_bytes mismatch");
+    if (!in_dev) return fail(PBF_ERR_INVALID, "null input");
+    f->pending = true;
+    if (f->alloc_words * 4 > nb_bytes)
+        HIP_TRY(hipMemsetAsync(reinterpret_cast<uint8_t*>(f->bitmap) + nb_bytes, 0, f->alloc_words * 4 - nb_bytes,
+                               f->stream));
+    HIP_TRY(hipMemcpyAsync(f->bitmap, in_dev, nb_bytes, hipMemcpyDeviceToDevice, f->stream));
+    f->pristine = false;
+    f->middle_dirty = f->tm.cspace != 0;
+    return PBF_OK;
+}
+
+int pbf_get_bitmap_device(pbf_filter_t* f, void* out_dev, uint64_t nb_bytes) {
+    LOCK(f);
+    int rc = enter(f);
+    if (rc) return rc;
+    if (nb_bytes != f->nb_bytes) return fail(PBF_ERR_INVALID, "nb_bytes mismatch");
+    if (!out_dev) return fail(PBF_ERR_INVALID, "null out");
+    rc = materialise(f);
+    if (rc) return rc;
+    f->pending = true;
+    HIP_TRY(hipMemcpyAsync(out_dev, f->bitmap, nb_bytes, hipMemcpyDeviceToDevice, f->stream));
+    return PBF_OK;
+}
+
+int pbf_copy_filter(pbf_filter_t* src, int dst_device, int flags, pbf_filter_t** out) {
+    if (!out) return fail(PBF_ERR_INVALID, "null out");
+    *out = nullptr;
+    if (flags & ~PBF_COPY_BOUNCE) return fail(PBF_ERR_INVALID, "bad copy flags");
+    LOCK(src);  // exclusive: no build or load of src while its bitmap is read
+    int rc = enter(src);
+    if (rc) return rc;
+    pbf_filter_t* dst = nullptr;
+    rc = pbf_create(dst_device, src->nb_bytes, src->k, &dst);
+    if (rc) return rc;
+    rc = copy_filter_into(src, dst, (flags & PBF_COPY_BOUNCE) != 0);
+    if (rc) {
+        const std::string msg = g_last_error;
+        pbf_destroy(dst);
+        return fail(rc, msg);
+    }
+    *out = dst;
+    return PBF_OK;
+}
+
 int pbf_popcount(pbf_filter_t* f, uint64_t* out) {
     LOCK(f);
     int rc = enter(f);
@@ -2575,12 +2719,15 @@ int pbf_may_contain(pbf_filter_t* f, const uint8_t* key, uint64_t len, int* out)
         // a built filter: readers share the handle and each runs on its reader stream
         std::shared_lock<std::shared_mutex> rl(f->mu);
         if (reader_ok(f, len)) {
-            int rc = enter(f);
-            if (rc) return rc;
             if (f->k == 0) {  // the AND over no bits (bloom_filter.py:71-74 runs no iteration)
                 *out = 1;
                 return PBF_OK;
             }
+            // the resident reader first: no HIP call on its path (no hipSetDevice either)
+            int rc = one_key_resident(f, key, len, out);
+            if (rc != kNotTaken) return rc;
+            rc = enter(f);
+            if (rc) return rc;
             hipStream_t rs = nullptr;
             HIP_TRY(reader_stream(f->device, &rs));
             return one_key_probe(f, key, len, out, rs, true);
@@ -2615,6 +2762,28 @@ int pbf_may_contain_set(pbf_filter_t* const* filters, uint32_t nfilters, const u
             }
         }
         if (ok) {
+            // every filter of one k (LsmStorage.get's usual set: product-sized SSTable filters,
+            // fp 0.001 -> k = 10), at most 64 of them: straight to the resident reader, no HIP call
+            const uint32_t k0 = filters[0]->k;
+            bool one_k = nfilters <= kSvcFilters && k0 > 0 && kmax_for(k0) > 0;
+            for (uint32_t i = 1; i < nfilters && one_k; ++i) one_k = filters[i]->k == k0;
+            if (one_k) {
+                SvcFilter sf[kSvcFilters];
+                for (uint32_t i = 0; i < nfilters; ++i) sf[i] = SvcFilter{filters[i]->bitmap, filters[i]->im};
+                uint64_t bits = 0;
+                bool taken = false;
+                const int rc = resident_probe(filters[0]->device, sf, nfilters, k0, key, len, &bits, &taken);
+                if (rc) return rc;
+                if (taken) {
+                    std::memset(out_bits, 0, (nfilters + 7) / 8);
+                    for (uint32_t i = 0; i < nfilters; ++i) {
+                        if ((bits >> i) & 1u) out_bits[i >> 3] |= uint8_t(1u << (i & 7));
+                        filters[i]->last_probe_mode = PBF_PROBE_DIRECT;
+                        filters[i]->last_probe_detail = PBF_DETAIL_ONE_KEY | PBF_DETAIL_SET | PBF_DETAIL_RESIDENT;
+                    }
+                    return PBF_OK;
+                }
+            }
             HIP_TRY(hipSetDevice(filters[0]->device));
             hipStream_t rs = nullptr;
             HIP_TRY(reader_stream(filters[0]->device, &rs));

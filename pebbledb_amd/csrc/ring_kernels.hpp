@@ -57,6 +57,10 @@ constexpr bool kRingBfe = PBF_RING_BFE;  // tile of a power-of-two position by o
 #define PBF_GATHER_BRANCH_FREE 1
 #endif
 constexpr bool kGatherBranchFree = PBF_GATHER_BRANCH_FREE;
+#ifndef PBF_RING_STORE_PHASE
+#define PBF_RING_STORE_PHASE 0
+#endif
+constexpr int kRingStorePhase = PBF_RING_STORE_PHASE;
 // Region capacity bound of the ring partition: tail (bytes) must stay below 2^16 although a
 // sub-chunk may append up to kps * k <= 8192 positions past lim (all to one tile: a duplicated
 // key) before the flush clamps it: 4 * (cap + 8192) < 2^16.
@@ -183,12 +187,17 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
     // flush stores a key load is followed by, and the wait for the next keys lets those stores
     // stay in flight instead of draining them (vmcnt counts loads and stores in issue order).
     const uint32_t lane = tid & 63u, wave = tid >> 6;
+    const uint32_t wave_u = __builtin_amdgcn_readfirstlane(wave);  // (wave-uniform branches)
     uint2* const wdesc = reinterpret_cast<uint2*>(lds + kRingHtWords * 4) + wave * 64;
     const uint32_t ring_own = tid << 7;   // ring byte offset of the owned tile
     const uint32_t rgn_own = tid * cap4;  // its region's byte offset in the workgroup's regions (< 2^32)
     const uint32_t q16 = (lane & 3u) << 4;
-    // the workgroup's 64-B dummy line after all regions (the host allocates G lines there)
-    const uint2 dummy = make_uint2(0u, uint32_t((uint64_t(pg.G) * B * cap - uint64_t(g) * B * cap) * 4 + g * 64));
+    // A flush with no group writes the workgroup's 64-B dummy line after all regions (the host
+    // allocates G lines there).  Its address is a 64-bit base of its own, chosen per wave (a
+    // scalar select), not a 32-bit offset from rgn: the regions of all workgroups may exceed 4 GiB.
+    char* const rgn_b = reinterpret_cast<char*>(rgn);
+    char* const dummy_b = reinterpret_cast<char*>(regions + uint64_t(pg.G) * B * cap) + uint64_t(g) * 64;
+    const uint2 dummy = make_uint2(0u, 0u);
     // A flush's first 32 groups (two store instructions) are read from the rings into registers
     // (take_groups) and stored after the next sub-chunk's hash (put_groups): the chain ht read ->
     // descriptor write -> descriptor read -> ring read -> store no longer holds the wave between
@@ -196,11 +205,13 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
     // at once (rare).
     struct Pending {
         uint4 x0, x1;    // pieces q of the wave's groups (lane >> 2) and 16 + (lane >> 2)
-        uint32_t a0, a1;  // their byte offsets in the workgroup's regions
+        uint32_t a0, a1;  // their byte offsets from `base`
+        char* base;       // the workgroup's regions, or its dummy line (no group: wave-uniform)
     };
     auto take_groups = [&](bool has, uint32_t hb, Pending& pd) {  // wave-uniform
         const uint64_t m = __builtin_amdgcn_ballot_w64(has);
-        const uint32_t total = uint32_t(__popcll(m));
+        const uint32_t total = __builtin_amdgcn_readfirstlane(uint32_t(__popcll(m)));
+        pd.base = total ? rgn_b : dummy_b;
         if (has) {
             const uint32_t slot = __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
             wdesc[slot] = make_uint2(ring_own | (hb & 64u), rgn_own + hb);
@@ -220,8 +231,8 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
         __builtin_amdgcn_wave_barrier();
     };
     auto put_groups = [&](const Pending& pd) {
-        st_stream<NT>(reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(rgn) + pd.a0), pd.x0);
-        st_stream<NT>(reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(rgn) + pd.a1), pd.x1);
+        st_stream<NT>(reinterpret_cast<uint32_t*>(pd.base + pd.a0), pd.x0);
+        st_stream<NT>(reinterpret_cast<uint32_t*>(pd.base + pd.a1), pd.x1);
     };
     auto write_groups = [&](bool has, uint32_t hb) {
         Pending pd;
@@ -321,7 +332,14 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
                 }
             }
             // the next sub-chunk's hash (the next batch's keys, at a batch's end), then this
-            // flush's stores
+            // flush's stores.  (PBF_RING_STORE_PHASE, A/B of the round-5 verdict's desynchronised
+            // store bursts: 1 = odd waves store before the hash, even waves after; 2 = one of the
+            // two store instructions before the hash, one after; 0 = both after, shipped.)
+            if constexpr (kRingStorePhase == 1) {
+                if (wave_u & 1u) put_groups(pd);
+            } else if constexpr (kRingStorePhase == 2) {
+                st_stream<NT>(reinterpret_cast<uint32_t*>(pd.base + pd.a0), pd.x0);
+            }
             if constexpr (u + 1 < P) {
                 hash_sub(s0 + kps, cw[F16 ? u + 1 : 0]);
             } else {
@@ -331,7 +349,13 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
                 }
                 hash_sub(c0 + uint64_t(P) * kps, cw[0]);
             }
-            put_groups(pd);
+            if constexpr (kRingStorePhase == 1) {
+                if (!(wave_u & 1u)) put_groups(pd);
+            } else if constexpr (kRingStorePhase == 2) {
+                st_stream<NT>(reinterpret_cast<uint32_t*>(pd.base + pd.a1), pd.x1);
+            } else {
+                put_groups(pd);
+            }
             ++j;
         };
         static_assert(P == 2, "two sub-chunks per batch");

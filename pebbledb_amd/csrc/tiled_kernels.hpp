@@ -743,7 +743,8 @@ __device__ __forceinline__ void tile_probe_body(uint32_t* smem, uint32_t b, cons
     // The region fills are loaded (and waited for) first; then the bitmap tile goes global -> LDS by
     // LDS-DMA while the word scan and the per-word table are built (no global load in between,
     // which would wait for the DMA too), and the stream starts once the DMA has landed.
-    const bool dma = PBF_TILE_DMA && (w0 & 3) == 0 && nw == W;
+    // (whole 1 KiB pieces only: tiles of 2^10..2^12 positions, W = 32..128 words, take load_tile)
+    const bool dma = PBF_TILE_DMA && (w0 & 3) == 0 && nw == W && W % 256 == 0;
     if (dma) {
         for (uint32_t q = tid; q < G; q += nt) fills[q] = (fill[uint64_t(b) * G + q] + 31) >> 5;  // words
         // (waits for the fill loads only)

@@ -52,3 +52,52 @@ def gather_hitmasks(per_filter: dict[int, np.ndarray], n_filters: int, n_keys: i
     for f, hm in per_filter.items():
         out[f] = np.unpackbits(np.asarray(hm, dtype=np.uint8), bitorder="little")[:n_keys].astype(bool)
     return out
+
+
+def exchange_bitmaps(dist, torch, n_filters: int, nb_bytes: int, export, load, device: int | None = None) -> dict:
+    """Give every rank every filter's bitmap, each built once by its owner (filters_for_rank):
+    the key-partitioned multi-GPU probe holds all of an LSM's filters on every GPU, and pebbledb
+    builds a filter once per SSTable (src/sstable.py:274, at flush src/lsm_storage.py:200-205)
+    while every get probes all of them (src/lsm_storage.py:164-179) — so the others' filters
+    arrive by replication, not by rebuilding.
+
+    export(g, t): write the rank's own filter g's nb_bytes-byte bitmap into the uint8 tensor t;
+    load(g, t): make filter g from t (another rank's).  With RCCL ('nccl') the tensors are on
+    `device` and the exchange is ONE all-gather when every rank owns the same number of filters
+    (8 filters over 1/2/4/8 GPUs), else one broadcast per filter from its owner; with gloo they
+    are host tensors.  Returns {"bytes_received": ..., "collective": ...}.  One-time setup of the
+    layout, never per step."""
+    world, rank = dist.get_world_size(), dist.get_rank()
+    on_dev = dist.get_backend() == "nccl"
+    dev = torch.device("cuda", device) if on_dev else torch.device("cpu")
+    owned = [filters_for_rank(n_filters, world, r) for r in range(world)]
+    mine = owned[rank]
+    if len({len(o) for o in owned}) == 1:
+        c = len(mine)
+        send = torch.empty(c * nb_bytes, dtype=torch.uint8, device=dev)
+        for i, g in enumerate(mine):
+            export(g, send[i * nb_bytes:(i + 1) * nb_bytes])
+        recv = torch.empty(world * c * nb_bytes, dtype=torch.uint8, device=dev)
+        if on_dev:
+            dist.all_gather_into_tensor(recv, send)
+        else:
+            dist.all_gather(list(recv.chunk(world)), send)
+        for r in range(world):
+            if r == rank:
+                continue
+            for i, g in enumerate(owned[r]):
+                o = (r * c + i) * nb_bytes
+                load(g, recv[o:o + nb_bytes])
+        return {"bytes_received": (world - 1) * c * nb_bytes,
+                "collective": f"all_gather ({'RCCL' if on_dev else 'gloo'})"}
+    buf = torch.empty(nb_bytes, dtype=torch.uint8, device=dev)
+    got = 0
+    for g in range(n_filters):
+        src = owner_of(g, n_filters, world)
+        if src == rank:
+            export(g, buf)
+        dist.broadcast(buf, src=src)
+        if src != rank:
+            load(g, buf.clone())
+            got += nb_bytes
+    return {"bytes_received": got, "collective": f"broadcast per filter ({'RCCL' if on_dev else 'gloo'})"}

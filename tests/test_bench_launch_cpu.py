@@ -93,6 +93,9 @@ def test_rank_plans_for_eight_gpus():
     assert all(a[1] == b[0] for a, b in zip(spans, spans[1:])) and all(b - a == 125_000_000 for a, b in spans)
     c5 = [bench.rank_plan("c5", world, r, r) for r in range(world)]
     assert all(p["filters"] == list(range(8)) and p["layout"] == "keys" for p in c5)
+    # each filter is built once, by one rank (the others receive it by replication)
+    assert sorted(g for p in c5 for g in p["builds"]) == list(range(8))
+    assert [p["builds"] for p in c5] == [[r] for r in range(world)]
     ks = [p["probe_keys"] for p in c5]
     assert ks[0][0] == 0 and ks[-1][1] == 100_000_000
     assert all(a[1] == b[0] for a, b in zip(ks, ks[1:]))

@@ -98,3 +98,60 @@ def test_gloo_world2_sharded_filters_equal_single_process():
         bm = o.build(4096, 6, PackedKeys.fixed(splitmix_hex_keys(77, a, b - a)))
         assert np.array_equal(np.frombuffer(masks[f], np.uint8), o.probe(bm, 6, probe))
         assert mat[f, a:b].all()  # members of filter f hit filter f
+
+
+def _exchange_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import torch
+    from oracle.oracle import COracle
+    from pebbledb_amd.keys import PackedKeys, splitmix_hex_keys
+    from pebbledb_amd.shard import exchange_bitmaps
+    o = COracle()
+    n_filters, kpf, nb, k = 8, 2000, 3001, 5
+    built = {}
+    for g in filters_for_rank(n_filters, world, rank):  # each filter built once, by its owner
+        a, b = key_range(g, kpf)
+        built[g] = o.build(nb, k, PackedKeys.fixed(splitmix_hex_keys(99, a, b - a)))
+    got = dict(built)
+
+    def export(g, t):
+        t.copy_(torch.from_numpy(built[g]))
+
+    def load(g, t):
+        assert g not in got
+        got[g] = t.numpy().copy()
+    info = exchange_bitmaps(dist, torch, n_filters, nb, export, load)
+    q.put((rank, {g: v.tobytes() for g, v in got.items()}, info))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_exchange_gives_every_rank_every_filter(world):
+    """The key-partitioned layout's replication (shard.exchange_bitmaps): each rank builds only
+    its own filters and receives the others' bitmaps — one all-gather when the ranks own equal
+    shares (world 2: 4 + 4), one broadcast per filter otherwise (world 3: 3 + 3 + 2) — and every
+    rank ends with the 8 filters bit-identical to building them itself."""
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_exchange_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    from oracle.oracle import COracle
+    from pebbledb_amd.keys import PackedKeys, splitmix_hex_keys
+    o = COracle()
+    want = {}
+    for g in range(8):
+        a, b = key_range(g, 2000)
+        want[g] = o.build(3001, 5, PackedKeys.fixed(splitmix_hex_keys(99, a, b - a))).tobytes()
+    for rank, got, info in res:
+        assert sorted(got) == list(range(8))
+        assert all(got[g] == want[g] for g in range(8)), rank
+        own = len(filters_for_rank(8, world, rank))
+        assert info["bytes_received"] == (8 - own) * 3001
+        assert info["collective"].startswith("all_gather" if world == 2 else "broadcast")

@@ -215,3 +215,98 @@ def test_config3_full_size_varlen_large_m(oracle):
     want_hm = oracle.probe(want, k, absent, omp=True)
     assert np.array_equal(h_all[n // 8:], want_hm)
     assert 30 < int(np.unpackbits(want_hm).sum()) < 300  # ~116 at these seeds (~70 expected)
+
+
+@pytest.mark.timeout(150)
+def test_ring_probe_with_regions_past_4gib(oracle):
+    """A ring-partition probe whose regions exceed 4 GiB (264M keys, k = 4, one pipeline of a
+    2^30-bit filter: G x B x cap x 4 B ~ 4.7 GB).  A flush with no complete group writes the
+    workgroup's dummy line after ALL regions; as a 32-bit offset from the workgroup's regions it
+    wrapped into another workgroup's live entries (round-5 advisor).  Tiled == direct probe over
+    the whole batch, members all hit, a sample == the oracle."""
+    n_m, nq, nb, k = 10_000_000, 264_000_000, 2 ** 27, 4
+    keys = dev_keys_hex(0x77, 0, nq)
+    bf = BloomFilter(nb, k)
+    bf.set_build_mode(PBF_BUILD_TILED)
+    bf.add_device_fixed(keys.data_ptr(), 16, n_m)
+    hm_t = torch.zeros(nq // 8, dtype=torch.uint8, device="cuda")
+    hm_d = torch.zeros(nq // 8, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    bf.set_probe_mode(PBF_PROBE_TILED)
+    bf.probe_device_fixed(keys.data_ptr(), 16, nq, hm_t.data_ptr())
+    bf.sync()
+    detail = bf.last_probe_detail
+    assert detail & _native.PBF_DETAIL_RING and (detail >> 16) == 1, hex(detail)  # one ring pipeline
+    sb = __import__("ctypes").c_uint64()
+    _native.check(_native.lib().pbf_scratch_bytes(0, __import__("ctypes").byref(sb)), "scratch")
+    assert sb.value > 4 * 2 ** 30 + 2 ** 28  # the regions alone pass 4 GiB
+    bf.set_probe_mode(PBF_PROBE_DIRECT)
+    bf.probe_device_fixed(keys.data_ptr(), 16, nq, hm_d.data_ptr())
+    bf.sync()
+    assert bool(torch.equal(hm_t, hm_d))
+    assert bool((hm_t[: n_m // 8] == 0xFF).all().item())
+    want = oracle.build(nb, k, PackedKeys.fixed(keys[: n_m * 16].cpu().numpy().reshape(-1, 16)), omp=True)
+    assert bf.bitmap() == want.tobytes()
+    s0 = nq - 1_000_000  # the batch's last workgroups: the regions' far end
+    qs = PackedKeys.fixed(keys[s0 * 16:].cpu().numpy().reshape(-1, 16))
+    assert np.array_equal(hm_t[s0 // 8:].cpu().numpy(), oracle.probe(want, k, qs, omp=True))
+    del keys, hm_t, hm_d
+    _native.check(_native.lib().pbf_trim(0), "trim")
+
+
+def test_replicate_and_device_bitmaps(oracle):
+    """BloomFilter.replicate (pbf_copy_filter: device to device, or through pinned host memory)
+    and the device-memory from_bytes / to_bytes (pbf_set_bitmap_device / pbf_get_bitmap_device):
+    each replica is the source's bitmap and k bit for bit (== the oracle), answers its probes
+    identically, and is independent of later changes to the source."""
+    n, nb, k = 300_000, 2 ** 20 + 12, 7
+    host = PackedKeys.fixed(splitmix_hex_keys(31, 0, n))
+    want = oracle.build(nb, k, host)
+    src = BloomFilter(nb, k)
+    src.add_many(host)
+    probes = PackedKeys.fixed(splitmix_hex_keys(31, n // 2, n))
+    want_hm = oracle.probe(want, k, probes)
+    for bounce in (False, True):
+        r = src.replicate(0, bounce=bounce)
+        assert r.nb_hash_functions == k and r.nb_bytes == nb and r.handle.value != src.handle.value
+        assert r.bitmap() == want.tobytes() and r == src
+        assert np.array_equal(r.may_contain_many(probes, packed=True), want_hm)
+        assert r.may_contain(f"{0:016x}") == src.may_contain(f"{0:016x}")
+    # the replica does not follow the source
+    r = src.replicate()
+    src.add_many(PackedKeys.fixed(splitmix_hex_keys(32, 0, 50_000)))
+    assert r.bitmap() == want.tobytes() and src.bitmap() != want.tobytes()
+    # a pristine (cleared) filter replicates to all zeros, including m > 2^32 (unreachable middle)
+    big = BloomFilter(2 ** 29 + 2 ** 16, 3)
+    big.add_many([f"k{i}" for i in range(1000)])
+    big.clear()
+    assert not any(big.replicate().bitmap())
+    big.add_many([f"k{i}" for i in range(1000)])
+    rb = big.replicate()
+    assert rb.bitmap() == big.bitmap() and rb.may_contain("k7") and not rb.may_contain("zz")
+    del big, rb
+    # device-memory to_bytes / from_bytes through a torch tensor
+    t = torch.zeros(nb, dtype=torch.uint8, device="cuda")
+    r.bitmap_to_device(t.data_ptr())
+    r.sync()
+    assert t.cpu().numpy().tobytes() == want.tobytes()
+    f2 = BloomFilter.from_device_bitmap(t.data_ptr(), nb, k, device=0,
+                                        stream=torch.cuda.current_stream().cuda_stream)
+    f2.sync()
+    assert f2.bitmap() == want.tobytes()
+    assert np.array_equal(f2.may_contain_many(probes, packed=True), want_hm)
+
+
+@pytest.mark.skipif(torch.cuda.device_count() < 2, reason="needs 2 GPUs (the driver's 8-GPU node)")
+def test_replicate_to_another_device(oracle):
+    """pbf_copy_filter across devices (peer copy over xGMI, and the pinned-host bounce)."""
+    n, nb, k = 200_000, 2 ** 22, 6
+    host = PackedKeys.fixed(splitmix_hex_keys(41, 0, n))
+    want = oracle.build(nb, k, host)
+    src = BloomFilter(nb, k, device=0)
+    src.add_many(host)
+    for bounce in (False, True):
+        r = src.replicate(1, bounce=bounce)
+        assert r.device == 1 and r.bitmap() == want.tobytes()
+        probes = PackedKeys.fixed(splitmix_hex_keys(41, n // 2, n))
+        assert np.array_equal(r.may_contain_many(probes, packed=True), oracle.probe(want, k, probes))

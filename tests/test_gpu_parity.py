@@ -199,6 +199,10 @@ CASES = [
     (123457, 6, "hex16", 200000), (2 ** 20 + 3, 10, "hex16", 300000), (2 ** 20, 8, "var", 100000),
     (77777, 17, "hex16", 20000), (5000, 33, "var", 3000), (4096, 40, "fixed7", 2000),
     (2 ** 24, 6, "fixed7", 500000), (2 ** 27, 6, "hex16", 1000000), (17971985, 10, "hex16", 1000000),
+    # one tile of 2^10..2^12 positions filling its 32..128 words exactly (ceil(m/32) == W): the tile
+    # test's bitmap load must not take the 1 KiB LDS-DMA pieces (round-5 advisor)
+    (125, 4, "hex16", 600), (128, 3, "var", 500), (253, 5, "hex16", 1200), (256, 4, "fixed7", 1500),
+    (509, 6, "var", 2500), (512, 3, "hex16", 3000),
 ]
 
 

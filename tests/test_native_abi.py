@@ -99,3 +99,21 @@ def test_placement_groups_of_a_multi_device_probe_without_gpu():
     rc, _, _ = plan([1, 1], [0, 3])
     assert rc == _native.PBF_ERR_INVALID and b"share a device" in L.pbf_last_error()
     assert plan([], []) [0] == 0
+
+
+def test_library_digest_is_the_trees_and_a_stale_library_is_refused(monkeypatch):
+    """The library carries the source_digest() it was compiled from (build_lib passes it in);
+    build.up_to_date() compares that, not file times, and _native.lib() refuses a library whose
+    digest is not the tree's, so a stale prebuilt .so can never be tested or benchmarked."""
+    from pebbledb_amd import build
+    assert build.embedded_digest(_native.LIB_PATH) == build.source_digest()
+    assert build.up_to_date()
+    L = _native.lib()
+    assert L.pbf_source_digest().decode() == build.source_digest()
+    monkeypatch.setattr(build, "source_digest", lambda: "0" * 64)
+    monkeypatch.setattr(_native, "_lib", None)
+    assert not build.up_to_date()
+    with pytest.raises(_native.NativeError, match="stale"):
+        _native.lib()
+    monkeypatch.undo()
+    assert _native.lib() is not None

@@ -169,6 +169,16 @@ for step in "$@"; do
            run bench 600 python bench.py
            prof prof 600 --steps 20 --warmup 5 --no-cpu-baseline --no-host-inclusive
            traffic c2 --steps 5 --warmup 2 ;;
+    pmc_c3_insts) for pc in "SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS" \
+                            "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_ANY SQ_WAIT_ANY GRBM_GUI_ACTIVE"; do
+                    i=$((${i:-0}+1))
+                    run pmc_c3_insts_$i 400 rocprofv3 --pmc $pc --kernel-trace --output-format csv -d gpurun_out/pmc_c3_insts_$i -o run -- python bench.py --config c3 --steps 2 --warmup 1 --no-cpu-baseline --no-host-inclusive
+                  done ;;
+    c5sim8) run c5sim_keys_w8 600 python bench.py --config c5 --sim-world 8 --sim-rank 0 --c5-layout keys --steps 10 --warmup 3 --no-host-c5 --no-cpu-baseline --no-compare
+            prof prof_c5sim_keys_w8 600 --config c5 --sim-world 8 --sim-rank 0 --c5-layout keys --steps 10 --warmup 3 --no-host-c5 --no-cpu-baseline --no-compare ;;
+    sl_c5) export PBF_BENCH_DEVICE=0 PBF_BENCH_BACKEND=gloo
+           run sl_c5_n2 300 python bench.py --gpus 2 --config c5 --steps 3 --warmup 1 --no-host-c5
+           unset PBF_BENCH_DEVICE PBF_BENCH_BACKEND ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
