@@ -315,7 +315,62 @@ def dropin_latency(device, reps=2000):
                         and out["pebbledb_amd"]["hits"] == out["reference_port"]["hits"])
     out["get_16_filters"] = get_set_latency(device)
     out["reader_threads"] = reader_threads(device)
+    out["batch_probe_with_gets"] = probe_with_gets(device)
     return out
+
+
+def probe_with_gets(device, reps=20):
+    """A batched C2 probe (20M keys against a 128 MiB filter, the tiled pipeline) alone and while
+    another thread issues per-key may_contain calls on a small L0 filter (LsmStorage.get traffic
+    beside a batch: the resident reader wave holds a CU slot while keys arrive, and the
+    partition's workgroups each take a whole CU).  Hit masks must be identical."""
+    import threading
+
+    import numpy as np
+    import torch
+    from pebbledb_amd import BloomFilter, _native
+    from pebbledb_amd.keys import splitmix_hex_keys_str
+    L = _native.lib()
+    n = 10_000_000
+    keys = torch.empty(2 * n * 16, dtype=torch.uint8, device=f"cuda:{device}")
+    _native.check(L.pbf_gen_splitmix_hex(device, None, keys.data_ptr(), SEED, 0, 2 * n), "gen")
+    big = BloomFilter(2 ** 27, 6, device=device)
+    big.add_device_fixed(keys.data_ptr(), 16, n)
+    hm = torch.zeros(2 * n // 8, dtype=torch.uint8, device=f"cuda:{device}")
+    small = BloomFilter.build_from_keys_and_fp_rate(splitmix_hex_keys_str(SEED, 0, 100_000), 0.001, device=device)
+    probes = splitmix_hex_keys_str(SEED, 50_000, 1000)
+    big.sync()
+
+    def batch():
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            big.probe_device_fixed(keys.data_ptr(), 16, 2 * n, hm.data_ptr())
+        big.sync()
+        return (time.perf_counter() - t0) / reps * 1e3
+
+    batch()
+    alone = batch()
+    ref = hm.cpu().numpy().copy()
+    stop = threading.Event()
+    calls = [0]
+
+    def gets():
+        i = 0
+        while not stop.is_set():
+            small.may_contain(probes[i % 1000])
+            i += 1
+        calls[0] = i
+    th = threading.Thread(target=gets)
+    th.start()
+    time.sleep(0.01)
+    t0 = time.perf_counter()
+    with_gets = batch()
+    dt = time.perf_counter() - t0
+    stop.set()
+    th.join()
+    return {"probe_ms_alone": round(alone, 4), "probe_ms_with_gets": round(with_gets, 4),
+            "gets_per_s_during": round(calls[0] / max(dt, 1e-9)),
+            "identical": bool(np.array_equal(ref, hm.cpu().numpy()))}
 
 
 def _native_lib():

@@ -77,7 +77,8 @@ class BloomFilter:
         self._pending: list[str] = []
         self._plock = threading.Lock()  # guards _pending (add / flush from several threads)
         self._h = None
-        self._hv = 0  # the handle as an int (the per-key fast path)
+        self._hv = 0  # the handle as an int
+        self._fast = 0  # _hv while no add is buffered: the per-key calls' handle (_pebblefast)
         # the part of a `bits` int outside the bitmap (bits >= 8*nb_bytes, or a negative int's
         # sign extension): the reference keeps the whole int (bloom_filter.py:31) and compares it
         # in __eq__ (:36), while only the low 8*nb_bytes bits are ever read or serialised
@@ -87,7 +88,7 @@ class BloomFilter:
             _native.check(_native.lib().pbf_create(self.device, nb_bytes, nb_hash_functions, ctypes.byref(h)),
                           "pbf_create")
             self._h = h
-            self._hv = h.value
+            self._hv = self._fast = h.value
         if bits:
             self._upload_int(bits)
 
@@ -126,6 +127,9 @@ class BloomFilter:
                 pend, self._pending = self._pending, []
             if pend:
                 self._add_packed(PackedKeys.from_strs(pend))
+            with self._plock:
+                if not self._pending:
+                    self._fast = self._hv
 
     def _add_packed(self, pk: PackedKeys) -> None:
         if pk.n == 0 or not self._require_modulus():
@@ -174,6 +178,7 @@ class BloomFilter:
     def bits(self, value: int) -> None:
         with self._plock:
             self._pending = []
+            self._fast = self._hv
         self._extra = 0
         if self.nb_bytes > 0:
             _native.check(_native.lib().pbf_clear(self._h), "pbf_clear")
@@ -213,6 +218,7 @@ class BloomFilter:
             self._require_modulus()
         with self._plock:
             self._pending.append(key)
+            self._fast = 0
             full = len(self._pending) >= _PENDING_FLUSH
         if full:
             self._flush()
@@ -220,10 +226,12 @@ class BloomFilter:
     def may_contain(self, key: str) -> bool:
         """bloom_filter.py:67-74 for one key (pbf_may_contain: answered by the device's resident
         reader wave, or one launch), called from C (_pebblefast) with the str's UTF-8 bytes."""
-        if self._pending:
+        f = self._fast
+        if not f and self._pending:
             self._flush()
-        if self._hv and self.nb_hash_functions > 0:
-            r = (_FAST or _fast()).may_contain(self._hv, key)
+            f = self._fast
+        if f:
+            r = (_FAST or _fast()).may_contain(f, key)
             if r is True or r is False:
                 return r
             if r != -100:  # (-100: not a str; the reference's key.encode raises below)
@@ -268,7 +276,7 @@ class BloomFilter:
         bf._pending = []
         bf._plock = threading.Lock()
         bf._h = None
-        bf._hv = 0
+        bf._hv = bf._fast = 0
         bf._extra = self._extra
         if self.nb_bytes > 0:
             self._flush()
@@ -276,7 +284,7 @@ class BloomFilter:
             _native.check(_native.lib().pbf_copy_filter(self._h, dev, _native.PBF_COPY_BOUNCE if bounce else 0,
                                                         ctypes.byref(h)), "pbf_copy_filter")
             bf._h = h
-            bf._hv = h.value
+            bf._hv = bf._fast = h.value
         return bf
 
     @classmethod
@@ -341,6 +349,7 @@ class BloomFilter:
     def clear(self) -> None:
         with self._plock:
             self._pending = []
+            self._fast = self._hv
         if self._h is not None:
             _native.check(_native.lib().pbf_clear(self._h), "pbf_clear")
 
@@ -492,43 +501,45 @@ def may_contain_multi(filters, keys, groups=None) -> np.ndarray:
     return out
 
 
-def may_contain_set(filters, key: str) -> list[bool]:
-    """``filters[i].may_contain(key)`` for every filter, in ONE launch per k (pbf_may_contain_set):
-    the per-key form of LsmStorage.get's bloom checks over its L0 and in-range level SSTables
-    (src/lsm_storage.py:164-179).  Filters may have any sizes; filters on several devices take
-    one launch per device."""
-    filters = list(filters)
+def may_contain_set_bits(filters, key: str) -> int:
+    """``may_contain_set`` as an int: bit i = ``filters[i].may_contain(key)``."""
     nf = len(filters)
     if not nf:
-        return []
-    # the common shape (LsmStorage.get: built filters, k > 0, one device, <= 64 of them): one C
-    # call (_pebblefast), no ctypes or numpy
-    dev0 = filters[0].device
+        return 0
+    # the common shape (LsmStorage.get: built filters on one device, <= 64 of them): one C call
+    # (_pebblefast), no ctypes or numpy; a buffered add (_fast == 0), a zero-size filter, filters
+    # on several devices (PBF_ERR_INVALID) or a non-str key (-100) take the general path below
     if nf <= 64:
-        hs = []
-        for bf in filters:
-            if bf._pending or bf.nb_hash_functions <= 0 or not bf._hv or bf.device != dev0:
-                break
-            hs.append(bf._hv)
-        else:
+        hs = [bf._fast for bf in filters]
+        if 0 not in hs:
             rc, bits = (_FAST or _fast()).may_contain_set(hs, key)
             if rc == 0:
-                return [(bits >> j) & 1 == 1 for j in range(nf)]
-            if rc != -100:
+                return bits
+            if rc not in (-100, _native.PBF_ERR_INVALID):
                 _native.check(rc, "pbf_may_contain_set")
     enc = key.encode("utf-8")
     native = _native_set(filters)
-    res = [True] * nf  # k == 0: the AND over no bits
+    bits = (1 << nf) - 1 - sum(1 << i for i in native)  # k == 0: the AND over no bits
     for dev in dict.fromkeys(filters[i].device for i in native):  # one call per device
         idx = [i for i in native if filters[i].device == dev]
         hs = (ctypes.c_void_p * len(idx))(*[filters[i]._h.value for i in idx])
         out = np.zeros((len(idx) + 7) // 8, dtype=np.uint8)
         _native.check(_native.lib().pbf_may_contain_set(hs, len(idx), enc, len(enc), _vp(out)),
                       "pbf_may_contain_set")
-        bits = np.unpackbits(out, bitorder="little")
+        got = np.unpackbits(out, bitorder="little")
         for j, i in enumerate(idx):
-            res[i] = bool(bits[j])
-    return res
+            bits |= int(got[j]) << i
+    return bits
+
+
+def may_contain_set(filters, key: str) -> list[bool]:
+    """``filters[i].may_contain(key)`` for every filter, in ONE launch per k (pbf_may_contain_set):
+    the per-key form of LsmStorage.get's bloom checks over its L0 and in-range level SSTables
+    (src/lsm_storage.py:164-179).  Filters may have any sizes; filters on several devices take
+    one launch per device."""
+    filters = list(filters)
+    bits = may_contain_set_bits(filters, key)
+    return [(bits >> j) & 1 == 1 for j in range(len(filters))]
 
 
 def probe_multi_device(filters, keys_ptr: int, n: int, hitmask_ptrs, key_len: int = 0, offsets_ptr: int = 0) -> None:

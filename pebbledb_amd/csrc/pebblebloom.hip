@@ -1890,15 +1890,23 @@ int resident_probe(int device, const SvcFilter* fs, uint32_t nf, uint32_t k, con
     ResidentReader* rr = ts.rr;
     SvcHead& hd = rr->host->head[ts.slot];
     SvcSlot& sl = rr->host->slot[ts.slot];
-    std::memcpy(sl.f, fs, size_t(nf) * sizeof(SvcFilter));
-    if (len) std::memcpy(sl.key, key, len);
+    // the body first (filters past the first, a key too long for the head), then head line 1
+    // (its tag req2 last), then line 0 (req last): the wave takes the request once both lines
+    // carry the new sequence (reader_service.hpp SvcHead)
+    if (nf > 1) std::memcpy(sl.f + 1, fs + 1, size_t(nf - 1) * sizeof(SvcFilter));
+    const bool inl = len <= kSvcInlineKey;
+    if (!inl) std::memcpy(sl.key, key, len);
     uint32_t seq = ts.seq + 1;
     if (seq == 0) seq = 1;
     ts.seq = seq;
+    if (inl && len > 16) std::memcpy(hd.key1, key + 16, len - 16);
+    __atomic_store_n(&hd.req2, seq, __ATOMIC_RELEASE);
     hd.nf = nf;
     hd.len = uint32_t(len);
     hd.k = k;
-    __atomic_store_n(&hd.req, seq, __ATOMIC_RELEASE);  // the body and the head's fields before it
+    hd.f0 = fs[0];
+    if (inl && len) std::memcpy(hd.key0, key, std::min<uint64_t>(len, 16));
+    __atomic_store_n(&hd.req, seq, __ATOMIC_RELEASE);
     int rc = PBF_OK;
     if (__atomic_load_n(&rr->host->state, __ATOMIC_ACQUIRE) == 0) {
         rc = resident_ensure(rr);

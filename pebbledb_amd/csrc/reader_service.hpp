@@ -4,14 +4,16 @@
 // A launch per key costs the host's launch path and the GPU's dispatch on every call (~9 us of
 // the ~12 us a may_contain took).  Instead ONE wave stays resident on a stream of its own while
 // keys arrive: host threads post requests into slots of a board in mapped, coherent pinned host
-// memory and the wave polls the slots' 16-byte heads over the bus (lane s reads slot s), answers
-// every posted request and writes the answer and the request's sequence number back.  The wave
+// memory and the wave polls the slots' 128-byte heads over the bus (one load round trip per
+// poll: 8 lanes per slot, the stop word beside them), answers every posted request and writes the
+// answer and the request's sequence number back.  The wave
 // leaves after `idle` ticks without a request (and after `life` ticks whatever happens, so it
 // never holds its queue for long), and on the board's stop word; the host relaunches it when a
 // request finds it gone (pebblebloom.hip: ResidentReader).
 //
-// Per request (one key against up to 64 filters sharing k, like k_may_contain_set): the key is
-// copied into LDS (one 16-B load per lane), lane s hashes seed s (MurmurHash3_x86_32, seeds
+// Per request (one key against up to 64 filters sharing k, like k_may_contain_set): the key
+// (from the head when it has at most 76 bytes, else one 16-B load per lane from the slot body)
+// goes into LDS, lane s hashes seed s (MurmurHash3_x86_32, seeds
 // 0..k-1), lane f gathers the k hashes from the other lanes and tests filter f's k bits, one
 // ballot is the answer.  Every load of host memory is volatile (the board changes under the
 // kernel: no load may be hoisted out of the poll loop or served from a cache), and the bitmap
@@ -29,6 +31,7 @@ namespace pbf {
 constexpr uint32_t kSvcSlots = 64;     // host threads with a slot (one lane each)
 constexpr uint32_t kSvcKeyMax = 1024;  // longer keys take the launch path
 constexpr uint32_t kSvcFilters = 64;   // filters per request (one lane each)
+constexpr uint32_t kSvcInlineKey = 76; // keys up to this many bytes travel in the head lines
 
 struct SvcFilter {  // 32 B
     const uint32_t* bm;
@@ -36,21 +39,30 @@ struct SvcFilter {  // 32 B
 };
 static_assert(sizeof(SvcFilter) == 32, "SvcFilter layout");
 
-// Slot s's request head (host-written, `req` last): one lane's poll reads it whole.
-struct SvcHead {
-    uint32_t req;  // sequence number of the posted request (never 0)
-    uint32_t nf;   // filters (1..kSvcFilters)
-    uint32_t len;  // key bytes (<= kSvcKeyMax)
-    uint32_t k;    // hash functions (1..32), shared by the request's filters
+// Slot s's request head: two 64-B lines, each written by the host with its sequence tag last
+// (req in line 0, req2 in line 1; x86 keeps stores in order, and a read of one line over the bus
+// returns a snapshot of it).  The wave reads both lines in its poll (8 lanes x 16 B per slot), and
+// a request is complete when req == req2: for a one-filter request with a key of up to
+// kSvcInlineKey bytes -- may_contain's -- the poll has brought everything the answer needs.
+struct alignas(64) SvcHead {
+    uint32_t req;        // line 0: sequence number of the posted request (never 0)
+    uint32_t nf;         // filters (1..kSvcFilters)
+    uint32_t len;        // key bytes (<= kSvcKeyMax)
+    uint32_t k;          // hash functions (1..32), shared by the request's filters
+    SvcFilter f0;        // filters[0]
+    uint8_t key0[16];    // key bytes [0, 16) (len <= kSvcInlineKey)
+    uint32_t req2;       // line 1: the same sequence number
+    uint8_t key1[60];    // key bytes [16, 76)
 };
+static_assert(sizeof(SvcHead) == 128, "SvcHead layout: two lines");
 
 struct SvcSlot {
     uint32_t ack;      // device: the sequence answered, stored after `bits`
     uint32_t pad0;
     uint64_t bits;     // device: bit f = filters[f] may contain the key
     uint8_t pad1[48];  // the body starts on its own 64-B line
-    SvcFilter f[kSvcFilters];
-    alignas(16) uint8_t key[kSvcKeyMax];
+    SvcFilter f[kSvcFilters];  // filters[1..nf) (filters[0] is in the head)
+    alignas(16) uint8_t key[kSvcKeyMax];  // keys longer than kSvcInlineKey
 };
 
 struct SvcBoard {
@@ -92,22 +104,28 @@ __device__ __forceinline__ bool svc_test(uint32_t h, uint32_t k, bool active, co
     return (acc & 1u) != 0u;
 }
 
-// One request of slot s: the key from host memory into LDS, one seed per lane, filter f on lane f.
+// One request of slot s, its head lines in LDS (hb, 32 words): the key into LDS (from the head,
+// or for a longer key one 16-B load per lane from the slot body), one seed per lane, filter f on
+// lane f (filter 0 from the head, the others from the slot body).
 __device__ __forceinline__ void svc_answer(SvcBoard* b, uint32_t s, uint32_t req, uint32_t nf, uint32_t len, uint32_t k,
-                                           uint32_t* kw) {
+                                           uint32_t* kw, const uint32_t* hb) {
     const uint32_t lane = threadIdx.x;
     SvcSlot* sl = b->slot + s;
-    // the key: 16 B per lane (the slot's key buffer is 16-B aligned and kSvcKeyMax = 64 x 16)
-    if (lane * 16 < len) {
+    if (len <= kSvcInlineKey) {
+        // key words 0..3 at head bytes 48..63, words 4..18 at bytes 68..127
+        if (lane < 19) kw[lane] = hb[lane < 4 ? 12 + lane : 17 + (lane - 4)];
+    } else if (lane * 16 < len) {  // 16 B per lane (the body's key buffer is 16-B aligned)
         const uint4 w = vload16(sl->key + lane * 16);
         kw[lane * 4] = w.x;
         kw[lane * 4 + 1] = w.y;
         kw[lane * 4 + 2] = w.z;
         kw[lane * 4 + 3] = w.w;
     }
-    // filter f's descriptor (issued beside the key loads)
     uint4 d0 = make_uint4(0, 0, 0, 0), d1 = d0;
-    if (lane < nf) {
+    if (lane == 0) {
+        d0 = make_uint4(hb[4], hb[5], hb[6], hb[7]);
+        d1 = make_uint4(hb[8], hb[9], hb[10], hb[11]);
+    } else if (lane < nf) {  // (issued beside the key loads)
         d0 = vload16(&sl->f[lane]);
         d1 = vload16(reinterpret_cast<const uint8_t*>(&sl->f[lane]) + 16);
     }
@@ -135,41 +153,70 @@ __device__ __forceinline__ void svc_answer(SvcBoard* b, uint32_t s, uint32_t req
         __hip_atomic_store(&sl->bits, uint64_t(bal), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(&sl->ack, req, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
-    __syncthreads();  // kw is rewritten by the next request
+    __syncthreads();  // kw and hb are rewritten by the next request
 }
 
 // The resident wave (one workgroup of 64 threads).  `id` is the launch's id (state while it
-// serves); ticks are wall-clock ticks (hipDeviceAttributeWallClockRate).
+// serves); ticks are wall-clock ticks (hipDeviceAttributeWallClockRate).  Each poll is ONE bus
+// round trip: the stop word and the used slots' head lines are loaded together (lane l reads
+// piece l & 7 of slot 8i + (l >> 3) in load i; the slot count of the previous poll decides how
+// many loads go out).
 __global__ void __launch_bounds__(64) k_reader_service(SvcBoard* b, uint32_t id, uint64_t idle_ticks, uint64_t life_ticks) {
     __shared__ uint32_t kw[kSvcKeyMax / 4 + 4];
-    const uint32_t lane = threadIdx.x;
-    uint32_t done = vload4(&b->slot[lane].ack);  // a relaunch resumes from the answered sequences
+    __shared__ uint32_t hb[32];
+    const uint32_t lane = threadIdx.x, grp = lane >> 3, piece = lane & 7;
+    constexpr int NI = kSvcSlots / 8;
+    // a relaunch resumes from the answered sequences
+    uint32_t done[NI];
+#pragma unroll
+    for (int i = 0; i < NI; ++i) done[i] = vload4(&b->slot[8 * i + grp].ack);
+    uint32_t nused = min(vload4(&b->nused), kSvcSlots);
     if (lane == 0) __hip_atomic_store(&b->state, id, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     const uint64_t t0 = wall_clock64();
     uint64_t t_last = t0;
     uint32_t served = 0;
     while (true) {
-        const uint4 ctl = vload16(&b->stop);  // stop, nused
+        const uint32_t ni = (nused + 7) >> 3;  // (wave-uniform)
+        const uint4 ctl = vload16(&b->stop);   // stop, nused
+        uint4 hv[NI];
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+            hv[i] = uint32_t(i) < ni ? vload16(reinterpret_cast<const uint8_t*>(&b->head[8 * i + grp]) + 16 * piece)
+                                     : make_uint4(0, 0, 0, 0);
         if (ctl.x) break;
-        const uint4 hd = lane < ctl.y ? vload16(&b->head[lane]) : make_uint4(done, 0, 0, 0);
-        const bool fresh = hd.x != done;
-        uint64_t pend = __ballot(fresh);
-        if (pend) {
+        nused = min(ctl.y, kSvcSlots);
+        bool any = false;
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            if (uint32_t(i) >= ni) break;
+            // the group's req (piece 0) and req2 (piece 4): complete when equal
+            const uint32_t req = __shfl(hv[i].x, int(lane & ~7u), 64);
+            const uint32_t req2 = __shfl(hv[i].x, int((lane & ~7u) | 4u), 64);
+            uint64_t pend = __ballot(piece == 0 && req != done[i] && req == req2);
             while (pend) {
-                const uint32_t s = uint32_t(__builtin_ctzll(pend));
+                const uint32_t g = uint32_t(__builtin_ctzll(pend)) >> 3;
                 pend &= pend - 1;
-                const uint32_t req = __shfl(hd.x, int(s), 64), nf = __shfl(hd.y, int(s), 64);
-                const uint32_t len = __shfl(hd.z, int(s), 64), k = __shfl(hd.w, int(s), 64);
-                // a malformed head (the host never posts one) is acknowledged with no hits
+                if (grp == g) reinterpret_cast<uint4*>(hb)[piece] = hv[i];
+                __syncthreads();
+                const uint32_t rq = hb[0], nf = hb[1], len = hb[2], k = hb[3];
+                const uint32_t s = 8 * uint32_t(i) + g;
+                // a malformed head (a request retracted by its host thread: nf = 0) is
+                // acknowledged with no hits, without reading any memory
                 if (nf >= 1 && nf <= kSvcFilters && len <= kSvcKeyMax && k >= 1 && k <= 32) {
-                    svc_answer(b, s, req, nf, len, k, kw);
-                } else if (lane == 0) {
-                    __hip_atomic_store(&b->slot[s].bits, uint64_t(0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                    __hip_atomic_store(&b->slot[s].ack, req, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+                    svc_answer(b, s, rq, nf, len, k, kw, hb);
+                } else {
+                    if (lane == 0) {
+                        __hip_atomic_store(&b->slot[s].bits, uint64_t(0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                        __hip_atomic_store(&b->slot[s].ack, rq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+                    }
+                    __syncthreads();
                 }
+                if (grp == g) done[i] = rq;
                 ++served;
+                any = true;
             }
-            if (fresh) done = hd.x;
+        }
+        if (any) {
             t_last = wall_clock64();
             continue;
         }

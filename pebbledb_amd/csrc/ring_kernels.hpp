@@ -57,10 +57,17 @@ constexpr bool kRingBfe = PBF_RING_BFE;  // tile of a power-of-two position by o
 #define PBF_GATHER_BRANCH_FREE 1
 #endif
 constexpr bool kGatherBranchFree = PBF_GATHER_BRANCH_FREE;
-#ifndef PBF_RING_STORE_PHASE
-#define PBF_RING_STORE_PHASE 0
+// When a flush's two group stores issue (A/B of the round-5 verdict's desynchronised store
+// bursts, profiles/r06/ab/): 0 = both after the next sub-chunk's hash; 1 = odd waves before it,
+// even waves after (so half the CU's waves reach the store phase at another time); 2 = one store
+// before, one after.  The build partition takes 1 (0.186-0.187 vs 0.191 ms per C2 build pass),
+// the probe partition 0 (1 and 2 measured 0.475 / 0.473 vs 0.472 ms).  PBF_RING_STORE_PHASE forces
+// one for both (A/B builds).
+#ifdef PBF_RING_STORE_PHASE
+constexpr int kRingStorePhaseBuild = PBF_RING_STORE_PHASE, kRingStorePhaseProbe = PBF_RING_STORE_PHASE;
+#else
+constexpr int kRingStorePhaseBuild = 1, kRingStorePhaseProbe = 0;
 #endif
-constexpr int kRingStorePhase = PBF_RING_STORE_PHASE;
 // Region capacity bound of the ring partition: tail (bytes) must stay below 2^16 although a
 // sub-chunk may append up to kps * k <= 8192 positions past lim (all to one tile: a duplicated
 // key) before the flush clamps it: 4 * (cap + 8192) < 2^16.
@@ -107,6 +114,7 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
 #define PBF_RING_PROBE_NT kNtProbePart
 #endif
     constexpr bool NT = PROBE ? PBF_RING_PROBE_NT : kNtBuildPart;
+    constexpr int kRingStorePhase = PROBE ? kRingStorePhaseProbe : kRingStorePhaseBuild;
     const uint32_t B = tm.nbuckets;  // <= 1024 = blockDim.x (host: ring_kps)
     const uint32_t shift = tm.tb;
     const uint32_t kps = pg.kps;  // keys per sub-chunk (<= 1024 threads)
@@ -210,7 +218,13 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
     };
     auto take_groups = [&](bool has, uint32_t hb, Pending& pd) {  // wave-uniform
         const uint64_t m = __builtin_amdgcn_ballot_w64(has);
-        const uint32_t total = __builtin_amdgcn_readfirstlane(uint32_t(__popcll(m)));
+#ifndef PBF_RING_UNIFORM_TOTAL
+#define PBF_RING_UNIFORM_TOTAL 1
+#endif
+        // (readfirstlane: the group count is known wave-uniform, so the descriptor selects and
+        // the loop over groups past 32 are scalar branches; A/B PBF_RING_UNIFORM_TOTAL=0)
+        const uint32_t total = PBF_RING_UNIFORM_TOTAL ? __builtin_amdgcn_readfirstlane(uint32_t(__popcll(m)))
+                                                      : uint32_t(__popcll(m));
         pd.base = total ? rgn_b : dummy_b;
         if (has) {
             const uint32_t slot = __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
@@ -332,9 +346,7 @@ __global__ void __launch_bounds__(1024) k_part_ring(KeySet ks, uint64_t n, int k
                 }
             }
             // the next sub-chunk's hash (the next batch's keys, at a batch's end), then this
-            // flush's stores.  (PBF_RING_STORE_PHASE, A/B of the round-5 verdict's desynchronised
-            // store bursts: 1 = odd waves store before the hash, even waves after; 2 = one of the
-            // two store instructions before the hash, one after; 0 = both after, shipped.)
+            // flush's stores (kRingStorePhase: when they issue)
             if constexpr (kRingStorePhase == 1) {
                 if (wave_u & 1u) put_groups(pd);
             } else if constexpr (kRingStorePhase == 2) {

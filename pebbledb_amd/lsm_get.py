@@ -30,7 +30,7 @@ from typing import NamedTuple, Sequence
 import numpy as np
 
 from . import _native
-from .bloom_filter import BloomFilter, _default_device, may_contain_multi, may_contain_set
+from .bloom_filter import BloomFilter, _default_device, may_contain_multi, may_contain_set_bits
 from .keys import PackedKeys
 
 
@@ -106,7 +106,7 @@ def candidates_one(key: str, level0: Sequence[BloomFilter], levels: Sequence[Seq
     one ``pbf_may_contain_set`` launch."""
     n0 = len(level0)
     in_range, tested = [], list(level0)
-    j = 0
+    j = n0
     for lvl in levels:
         for t in lvl:
             if t.first_key <= key <= t.last_key:
@@ -115,7 +115,22 @@ def candidates_one(key: str, level0: Sequence[BloomFilter], levels: Sequence[Seq
             j += 1
     if not tested:
         return []
-    hits = may_contain_set(tested, key)
-    out = [t for t in range(n0) if hits[t]]
-    out += [n0 + j for r, j in enumerate(in_range) if hits[n0 + r]]
+    bits = may_contain_set_bits(tested, key)
+    out = list(_set_bits(bits & ((1 << n0) - 1)))
+    if in_range:
+        out += [in_range[r] for r in _set_bits(bits >> n0)]
     return out
+
+
+_SET_BITS: dict = {}
+
+
+def _set_bits(b: int) -> tuple:
+    """The indices of b's set bits, ascending (memoised: a get's hit pattern over its L0 and
+    in-range tables repeats)."""
+    r = _SET_BITS.get(b)
+    if r is None:
+        r = tuple(i for i in range(b.bit_length()) if b >> i & 1)
+        if len(_SET_BITS) < 1 << 16:
+            _SET_BITS[b] = r
+    return r

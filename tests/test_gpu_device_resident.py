@@ -274,7 +274,7 @@ def test_replicate_and_device_bitmaps(oracle):
         assert r.may_contain(f"{0:016x}") == src.may_contain(f"{0:016x}")
     # the replica does not follow the source
     r = src.replicate()
-    src.add_many(PackedKeys.fixed(splitmix_hex_keys(32, 0, 50_000)))
+    src.add_many(PackedKeys.fixed(splitmix_hex_keys(31, 10 ** 9, 50_000)))
     assert r.bitmap() == want.tobytes() and src.bitmap() != want.tobytes()
     # a pristine (cleared) filter replicates to all zeros, including m > 2^32 (unreachable middle)
     big = BloomFilter(2 ** 29 + 2 ** 16, 3)

@@ -30,6 +30,11 @@ def test_one_key_may_contain_matches_oracle(oracle):
     d, o = varlen_keys(5, 0, 3000)
     members = PackedKeys(d, 3000, offsets=o)
     extra = ["", "é", "ключ", "🔑" * 3, "x" * 5000, "y" * 4096, "z" * 4097]
+    # the resident reader's head carries keys of up to 76 bytes; longer ones (to 1 KiB) come from
+    # the slot body, longer still take the launch
+    extra += [("%d-" % n) + "k" * (n - len("%d-" % n)) for n in (15, 16, 17, 47, 48, 49, 75, 76, 77, 78, 100, 1023,
+                                                                   1024, 1025)]
+    extra += ["é" * 38, "é" * 39]  # 76 / 78 UTF-8 bytes
     keys = _strs(members) + extra
     probes = keys + [s + "!" for s in keys[:1500]] + ["absent-%d" % i for i in range(500)]
     for nb, k in ((2 ** 14, 6), (100_003, 7), (777, 3), (64, 40)):

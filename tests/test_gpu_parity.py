@@ -414,6 +414,20 @@ for nb, pk, q in ((2 ** 27, fx, probes), (3 * 2 ** 25, vr, vr), (2 ** 21, fx, pr
     assert bf.last_probe_mode == 2 and bf.last_build_mode == 2
     if os.environ.get('PBF_PART') == 'sort':  # exact k = 6: packed entries unless disabled
         assert bool(bf.last_build_detail & _native.PBF_DETAIL_PACKED) == (os.environ.get('PBF_PK3') != '0'), hex(bf.last_build_detail)
+# the spill path of a shared multi-filter pipeline (every spilled position tested against each
+# filter of the set, ring_kernels.hpp spill_one / tiled_kernels.hpp spill_probe): three filters of
+# 16 tiles whose rings overflow constantly, against the oracle
+from pebbledb_amd import may_contain_multi
+sets = [PackedKeys.fixed(np.concatenate([splitmix_hex_keys(40, f * 10 ** 6, 150000), same])) for f in range(3)]
+wants = [o.build(2 ** 21, 6, m, omp=True) for m in sets]
+fs = []
+for m in sets:
+    bf = BloomFilter(2 ** 21, 6); bf.set_build_mode(2); bf.add_many(m); bf.set_probe_mode(2)
+    fs.append(bf)
+got = may_contain_multi(fs, probes)
+assert fs[0].last_probe_mode == 2 and (fs[0].last_probe_detail >> 8) & 0xFF == 3, hex(fs[0].last_probe_detail)
+for i in range(3):
+    assert np.array_equal(got[i], o.probe(wants[i], 6, probes, omp=True)), i
 print('ok')
 """
 

@@ -179,6 +179,8 @@ for step in "$@"; do
     sl_c5) export PBF_BENCH_DEVICE=0 PBF_BENCH_BACKEND=gloo
            run sl_c5_n2 300 python bench.py --gpus 2 --config c5 --steps 3 --warmup 1 --no-host-c5
            unset PBF_BENCH_DEVICE PBF_BENCH_BACKEND ;;
+    diag_repl) run diag_repl 300 python tools/diag/replicate_check.py
+               run diag_repl_pytest 300 python -u -m pytest tests/test_gpu_device_resident.py -m gpu -x -v -rf --timeout 150 --timeout-method thread -k "replicate" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
