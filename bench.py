@@ -341,12 +341,20 @@ def probe_with_gets(device, reps=20):
     probes = splitmix_hex_keys_str(SEED, 50_000, 1000)
     big.sync()
 
+    st = torch.cuda.ExternalStream(big.stream)
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(reps)]
+
     def batch():
+        # wall time per probe, and the probes' own GPU time (HIP events around each on the
+        # filter's stream: host-side delays between enqueues do not count there)
         t0 = time.perf_counter()
-        for _ in range(reps):
+        for e in ev:
+            e[0].record(st)
             big.probe_device_fixed(keys.data_ptr(), 16, 2 * n, hm.data_ptr())
+            e[1].record(st)
         big.sync()
-        return (time.perf_counter() - t0) / reps * 1e3
+        wall = (time.perf_counter() - t0) / reps * 1e3
+        return wall, sum(e[0].elapsed_time(e[1]) for e in ev) / reps
 
     batch()
     alone = batch()
@@ -368,7 +376,8 @@ def probe_with_gets(device, reps=20):
     dt = time.perf_counter() - t0
     stop.set()
     th.join()
-    return {"probe_ms_alone": round(alone, 4), "probe_ms_with_gets": round(with_gets, 4),
+    return {"probe_ms_alone": round(alone[1], 4), "probe_ms_with_gets": round(with_gets[1], 4),
+            "wall_ms_per_probe_alone": round(alone[0], 4), "wall_ms_per_probe_with_gets": round(with_gets[0], 4),
             "gets_per_s_during": round(calls[0] / max(dt, 1e-9)),
             "identical": bool(np.array_equal(ref, hm.cpu().numpy()))}
 

@@ -135,6 +135,8 @@ constexpr int kProbeStage1 = 2;
 // Measured (profiles/r02/s5): the counting-sort PROBE partition prefers 512 (C3 probe 17.4 ->
 // 16.0 ms: the gather's per-workgroup key bitmap and run tables halve, more gather workgroups
 // fit a CU), the ring partition 256 (C2 probe 0.586 -> 0.604 ms at 512).
+bool resident_live(int device);  // (the resident one-key reader below)
+
 uint64_t part_max_groups(bool sort_probe) {
     static const long long v = [] {
         const char* e = std::getenv("PBF_PART_G");
@@ -307,6 +309,7 @@ struct pbf_filter {
     std::atomic<uint32_t> last_probe_detail{0};   // PBF_DETAIL_* of the last probe
     uint32_t last_build_detail = 0;  // PBF_DETAIL_* | (kps / 256) << 12 of the last tiled build
     Scratch* sc = nullptr;           // leased for the current call
+    bool spare_cu = false;           // the current tiled call plans around a resident reader (groups_cap)
     uint64_t* dpop = nullptr;
     hipEvent_t ev = nullptr;       // stream joins of multi-filter probes
     hipEvent_t wait_ev = nullptr;  // pbf_wait_stream: the caller's stream -> this stream
@@ -659,9 +662,19 @@ void set_gather(PartPlan& pl, uint32_t B, uint32_t row, uint32_t nf = 1) {
     }
 }
 
-PartPlan plan_ring(uint32_t B, uint32_t k, uint64_t n, uint32_t kps, bool probe, double share, uint32_t nf = 1) {
+// Partition workgroups each take a whole CU (all of its LDS).  Workgroups are dealt round-robin
+// over the 8 XCDs (32 CUs each): while the device's resident one-key reader holds a CU slot
+// (reader_service.hpp), 256 workgroups put 32 on its XCD, and one of them waits for a second
+// round.  `spare`: plan for 31 per XCD then.
+uint64_t groups_cap(bool sort_probe, bool spare) {
+    const uint64_t g = part_max_groups(sort_probe);
+    return spare && g >= 256 ? g / 256 * 248 : g;
+}
+
+PartPlan plan_ring(uint32_t B, uint32_t k, uint64_t n, uint32_t kps, bool probe, double share, uint32_t nf = 1,
+                   bool spare = false) {
     PartPlan pl{};
-    const uint64_t G0 = std::min<uint64_t>(part_max_groups(false), std::max<uint64_t>(1, (n + kps - 1) / kps));
+    const uint64_t G0 = std::min<uint64_t>(groups_cap(false, spare), std::max<uint64_t>(1, (n + kps - 1) / kps));
     uint64_t kpw = (n + G0 - 1) / G0;
     kpw = ((kpw + kps - 1) / kps) * kps;
     pl.pg.G = uint32_t(std::max<uint64_t>(1, (n + kpw - 1) / kpw));
@@ -697,7 +710,8 @@ bool pk3_enabled() {
     return v;
 }
 
-PartPlan plan_partition(uint32_t B, uint32_t k, int km, uint64_t n, bool probe, double share, uint32_t nf) {
+PartPlan plan_partition(uint32_t B, uint32_t k, int km, uint64_t n, bool probe, double share, uint32_t nf,
+                        bool spare = false) {
     PartPlan pl{};
     const size_t per_entry = probe ? 6 : 4;  // stage u32 (+ u16 tile id for probes)
     const size_t fixed = size_t(3 * B + 1 + 16) * 4;
@@ -718,7 +732,7 @@ PartPlan plan_partition(uint32_t B, uint32_t k, int km, uint64_t n, bool probe, 
     if (pl.pk3) scap -= scap % 3;  // windows hold whole packed words
     pl.pg.scap = uint32_t(scap);
     pl.lds_part = fixed + size_t(scap) * per_entry;
-    const uint64_t G0 = std::min<uint64_t>(part_max_groups(probe), std::max<uint64_t>(1, (n + kps - 1) / kps));
+    const uint64_t G0 = std::min<uint64_t>(groups_cap(probe, spare), std::max<uint64_t>(1, (n + kps - 1) / kps));
     uint64_t kpw = (n + G0 - 1) / G0;
     kpw = ((kpw + kps - 1) / kps) * kps;
     pl.pg.G = uint32_t(std::max<uint64_t>(1, (n + kpw - 1) / kpw));
@@ -762,16 +776,18 @@ double busiest_tile_share(const TileMap& tm) {
 }
 
 // nf: filters one ring gather serves at once (a multi-filter probe).
-PartPlan plan_for(const TileMap& tm, uint32_t k, int km, uint64_t n, bool probe, uint32_t nf = 1) {
+// spare: leave a CU per XCD to the resident reader (groups_cap), decided once per call
+// (pbf_filter::spare_cu) so a probe's batch split and its pipelines plan alike.
+PartPlan plan_for(const TileMap& tm, uint32_t k, int km, uint64_t n, bool probe, uint32_t nf = 1, bool spare = false) {
     const uint32_t B = tm.nbuckets;
     const double share = busiest_tile_share(tm);
     if (const uint32_t kps = ring_kps(B, k, probe, tm.tb)) {
-        const PartPlan pl = plan_ring(B, k, n, kps, probe, share, probe ? nf : 1);
+        const PartPlan pl = plan_ring(B, k, n, kps, probe, share, probe ? nf : 1, spare);
         // lim / tail are 16-bit byte counts in LDS (cap <= kRingMaxCap); entry offsets within a
         // workgroup's regions are 32-bit (B * cap < 2^32)
         if (pl.pg.cap <= kRingMaxCap && uint64_t(B) * pl.pg.cap < (uint64_t(1) << 32)) return pl;
     }
-    return plan_partition(B, k, km, n, probe, share, probe ? nf : 1);
+    return plan_partition(B, k, km, n, probe, share, probe ? nf : 1, spare);
 }
 
 // The ring partition kernel for (k, key layout): with the seed count fixed at compile time
@@ -821,7 +837,7 @@ int run_tiled(pbf_filter_t* f, const Batch& b) {
     const TileMap& tm = f->tm;
     const uint32_t B = tm.nbuckets;
     const uint32_t k = f->k;
-    const PartPlan pl = plan_for(tm, k, b.km, b.n, false);
+    const PartPlan pl = plan_for(tm, k, b.km, b.n, false, 1, f->spare_cu);
     const PartGeom& pg = pl.pg;
     // (+ the ring partition's 64-B dummy line per workgroup after the regions)
     HIP_TRY(f->sc->regions.ensure(size_t(pg.G) * B * pg.cap * 4 + size_t(pg.G) * 64));
@@ -892,7 +908,7 @@ int run_tiled_probe_set(pbf_filter_t* f, pbf_filter_t* const* fs, uint32_t nf, c
     const TileMap& tm = f->tm;
     const uint32_t B = tm.nbuckets;
     const uint32_t k = f->k;
-    const PartPlan pl = plan_for(tm, k, b.km, b.n, true, nf);
+    const PartPlan pl = plan_for(tm, k, b.km, b.n, true, nf, f->spare_cu);
     const PartGeom& pg = pl.pg;
     f->last_probe_detail = (pg.ring ? PBF_DETAIL_RING : PBF_DETAIL_SORT) | (nf << 8);
     HIP_TRY(sc->regions.ensure(size_t(pg.G) * B * pg.cap * 4 + size_t(pg.G) * 64));
@@ -1043,7 +1059,7 @@ bool want_tiled_probe(pbf_filter_t* f, uint64_t n) {
 uint64_t tiled_probe_batch(pbf_filter_t* f, int km, uint32_t nf, uint64_t total) {
     const uint32_t k = f->k;
     auto fits = [&](uint64_t m) {
-        const PartPlan pl = plan_for(f->tm, k, km, m, true, nf);
+        const PartPlan pl = plan_for(f->tm, k, km, m, true, nf, f->spare_cu);
         // the tile test addresses a region word by a u32 global index (run_tiled_probe_set)
         return pl.lds_gather <= 156 * 1024 && pl.pg.cap <= 65535 &&
                uint64_t(pl.pg.G) * f->tm.nbuckets * (pl.pg.cap / 32) < (uint64_t(1) << 32);
@@ -1070,6 +1086,7 @@ uint64_t tiled_probe_batch(pbf_filter_t* f, int km, uint32_t nf, uint64_t total)
 int add_device(pbf_filter_t* f, const Batch& b) {
     if (b.n == 0 || f->k == 0) return PBF_OK;
     if (want_tiled(f, b.n)) {
+        f->spare_cu = resident_live(f->device);
         // positions are counted in u32 inside one pipeline, and a region holds < 2^24 entries
         // (the partitions' 24-bit region addressing): batch very large inputs
         const double share = busiest_tile_share(f->tm);
@@ -1091,6 +1108,7 @@ int probe_device(pbf_filter_t* f, const Batch& b, uint8_t* hitmask_dev) {
     int rc = materialise(f);
     if (rc) return rc;
     if (want_tiled_probe(f, b.n)) {
+        f->spare_cu = resident_live(f->device);
         const uint64_t per = tiled_probe_batch(f, b.km, 1, b.n);
         for (uint64_t i0 = 0; i0 < b.n; i0 += per) {
             rc = run_tiled_probe(f, slice(b, i0, std::min<uint64_t>(per, b.n - i0)), hitmask_dev + i0 / 8);
@@ -1227,6 +1245,7 @@ int probe_multi_device(pbf_filter_t* const* fs, uint32_t nf, const Batch& b, uin
         }
     }
     if (shared_probe(fs, nf, b.n)) {
+        f0->spare_cu = resident_live(f0->device);
         const uint64_t per = tiled_probe_batch(f0, b.km, std::min<uint32_t>(nf, kMaxProbeSet), b.n);
         for (uint64_t i0 = 0; i0 < b.n; i0 += per) {
             const Batch c = slice(b, i0, std::min<uint64_t>(per, b.n - i0));
@@ -1821,7 +1840,16 @@ ResidentReader* resident_reader(int device) {
     } while (false);
     (void)hipGetLastError();
     g_resident[device] = rr;
+    if (rr && device >= 0 && device < 64) g_resident_fast[device].store(rr, std::memory_order_release);
     return rr;
+}
+
+// Whether the device's resident reader wave is on the GPU now (lock-free: the board's state word).
+std::atomic<ResidentReader*> g_resident_fast[64];
+bool resident_live(int device) {
+    if (device < 0 || device >= 64) return false;
+    ResidentReader* rr = g_resident_fast[device].load(std::memory_order_acquire);
+    return rr && rr->host && __atomic_load_n(&rr->host->state, __ATOMIC_ACQUIRE) != 0;
 }
 
 // A wave serving rr's board: launch one unless the last launch is still running (or queued).

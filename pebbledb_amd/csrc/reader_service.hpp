@@ -82,6 +82,17 @@ __device__ __forceinline__ uint4 vload16(const void* p) {
 }
 __device__ __forceinline__ uint32_t vload4(const void* p) { return *reinterpret_cast<const volatile uint32_t*>(p); }
 
+// The answer: ack and bits in ONE 16-byte store to the slot's first 16 bytes (a single bus write,
+// so the host never sees the new ack with the old bits) -- not a release at system scope, which
+// compiles to an L2 write-back (buffer_wbl2) of this XCD's whole L2 per answer: with ~200k gets/s
+// that slowed a concurrent batched probe by 40% (profiles/r06/s3).  The board is coherent host
+// memory, which the GPU does not cache.
+__device__ __forceinline__ void svc_ack(SvcSlot* sl, uint32_t req, uint64_t bits) {
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    const v4u x = {req, 0u, uint32_t(bits), uint32_t(bits >> 32)};
+    *reinterpret_cast<volatile v4u*>(sl) = x;
+}
+
 // Filter fd's k bits (lanes f < nf) for the hashes held by lanes 0..k-1 (k <= KMAX): every
 // lane takes part in the shuffles (a lane reading an inactive lane's register gets no data), then
 // the k loads of a filter go out together.
@@ -149,10 +160,7 @@ __device__ __forceinline__ void svc_answer(SvcBoard* b, uint32_t s, uint32_t req
                      : k <= 16 ? svc_test<16>(h, k, act, fd)
                                : svc_test<32>(h, k, act, fd);
     const unsigned long long bal = __ballot(hit);
-    if (lane == 0) {
-        __hip_atomic_store(&sl->bits, uint64_t(bal), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(&sl->ack, req, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
+    if (lane == 0) svc_ack(sl, req, uint64_t(bal));
     __syncthreads();  // kw and hb are rewritten by the next request
 }
 
@@ -205,10 +213,7 @@ __global__ void __launch_bounds__(64) k_reader_service(SvcBoard* b, uint32_t id,
                 if (nf >= 1 && nf <= kSvcFilters && len <= kSvcKeyMax && k >= 1 && k <= 32) {
                     svc_answer(b, s, rq, nf, len, k, kw, hb);
                 } else {
-                    if (lane == 0) {
-                        __hip_atomic_store(&b->slot[s].bits, uint64_t(0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                        __hip_atomic_store(&b->slot[s].ack, rq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-                    }
+                    if (lane == 0) svc_ack(b->slot + s, rq, 0);
                     __syncthreads();
                 }
                 if (grp == g) done[i] = rq;
@@ -226,7 +231,7 @@ __global__ void __launch_bounds__(64) k_reader_service(SvcBoard* b, uint32_t id,
     }
     if (lane == 0) {
         __hip_atomic_store(&b->served, served, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(&b->state, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&b->state, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
