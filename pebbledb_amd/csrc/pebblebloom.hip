@@ -62,27 +62,67 @@ int fail(int code, const std::string& msg) {
         CHECK_LAUNCH();             \
     } while (0)
 
+// Every stream the library queues work on (the filter and reader stream pools, the encoder's),
+// per device: a buffer's users are done once these are (not a device-wide sync, which would also
+// wait for the resident reader's wave, up to its 200 ms life).
+std::mutex g_lib_streams_mu;
+std::map<int, std::vector<hipStream_t>> g_lib_streams;
+void register_stream(int device, hipStream_t s) {
+    std::lock_guard<std::mutex> lock(g_lib_streams_mu);
+    g_lib_streams[device].push_back(s);
+}
+hipError_t sync_library_streams() {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    std::vector<hipStream_t> ss;
+    {
+        std::lock_guard<std::mutex> lock(g_lib_streams_mu);
+        ss = g_lib_streams[dev];
+    }
+    for (hipStream_t s : ss)
+        if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+    return hipStreamSynchronize(nullptr);
+}
+
+// Device working memory from the device's stream-ordered pool (hipMallocAsync / hipFreeAsync on
+// the null stream): hipFree and hipDeviceSynchronize wait for every kernel on the device, the
+// resident reader's too (measured: tools/microbench/cumask_block.hip), the pool's calls do not.
 struct DevBuf {
     void* p = nullptr;
     size_t bytes = 0;
+    bool pooled = false;
     hipError_t ensure(size_t want) {
         if (want <= bytes) return hipSuccess;
         if (p) {
-            // growth only: the old buffer may still be read by queued work on any stream
-            hipError_t s = hipDeviceSynchronize();
+            // growth only: the old buffer may still be read by queued work on the library's streams
+            hipError_t s = sync_library_streams();
             if (s != hipSuccess) return s;
-            (void)hipFree(p);
+            release();
         }
-        p = nullptr;
-        bytes = 0;
-        hipError_t e = hipMalloc(&p, want);
+        hipError_t e = hipMallocAsync(&p, want, nullptr);
+        pooled = e == hipSuccess;
+        if (pooled) {
+            e = hipStreamSynchronize(nullptr);  // usable from every stream
+        } else {
+            (void)hipGetLastError();
+            e = hipMalloc(&p, want);
+        }
         if (e == hipSuccess) bytes = want;
         return e;
     }
     void release() {
-        if (p) (void)hipFree(p);
+        if (p) {
+            if (pooled) {
+                (void)hipFreeAsync(p, nullptr);
+                (void)hipStreamSynchronize(nullptr);
+            } else {
+                (void)hipFree(p);
+            }
+        }
         p = nullptr;
         bytes = 0;
+        pooled = false;
     }
 };
 
@@ -471,6 +511,7 @@ hipError_t pooled_stream(int device, hipStream_t* out) {
             break;
         }
         pool.first.push_back(st);
+        register_stream(device, st);
     }
     *out = pool.first[pool.second++ % pool.first.size()];
     return hipSuccess;
@@ -1729,6 +1770,7 @@ hipError_t reader_stream(int device, hipStream_t* out) {
             break;
         }
         pool.push_back(st);
+        register_stream(device, st);
     }
     *out = mine[device] = pool[next++ % pool.size()];
     return hipSuccess;
@@ -1736,8 +1778,9 @@ hipError_t reader_stream(int device, hipStream_t* out) {
 
 // ---------------------------------------------------------------- resident one-key reader
 // (reader_service.hpp) One board per device in mapped, coherent pinned memory, one resident
-// wave serving it on a stream with a CU mask (a stream with a CU mask gets a hardware queue of
-// its own, so the resident wave never holds up other streams' work), one slot per host thread.
+// wave serving it on a high-priority non-blocking stream (it gets a hardware queue of its own,
+// so the resident wave never holds up other streams' work, and the null stream does not wait for
+// it), one slot per host thread.
 // PBF_RESIDENT_READER=0 sends every one-key probe through the per-key launch instead;
 // PBF_RESIDENT_IDLE_US (default 2000) is how long the wave waits for a key before it leaves.
 struct ResidentReader {
@@ -1770,6 +1813,7 @@ bool resident_enabled() {
 
 std::mutex g_resident_mu;
 std::map<int, ResidentReader*> g_resident;  // never freed: a wave may still poll its board at exit
+std::atomic<ResidentReader*> g_resident_fast[64];  // (the same, lock-free lookups)
 
 // At exit: every resident wave is told to leave and given a few milliseconds to do so (it
 // leaves by itself after its idle time anyway).
@@ -1786,6 +1830,12 @@ void resident_shutdown() {
         if (!rr || !rr->host) continue;
         while (__atomic_load_n(&rr->host->state, __ATOMIC_ACQUIRE) != 0 &&
                std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(20)) {
+        }
+        // and the launch itself has completed (its end is recorded on rr->done), so no kernel of
+        // the library is still in flight when the runtime (and a profiler's tool) tears down
+        std::lock_guard<std::mutex> lock(rr->mu);
+        while (rr->launched && !event_done(rr->done) &&
+               std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(50)) {
         }
     }
 }
@@ -1813,10 +1863,15 @@ ResidentReader* resident_reader(int device) {
             (void)hipHostFree(h);
             break;
         }
-        std::vector<uint32_t> mask((size_t(ncu) + 31) / 32, ~0u);
-        if (ncu % 32) mask.back() = (1u << (ncu % 32)) - 1u;
+        // A high-priority non-blocking stream: it gets a hardware queue of its own (the pool
+        // streams' kernels are not held up behind the wave) and the null stream does not wait
+        // for it.  (A CU-masked stream also has its own queue, but hipExtStreamCreateWithCUMask
+        // makes a BLOCKING stream: null-stream work -- torch's default stream -- waited for the
+        // wave; tools/microbench/cumask_block.hip, profiles/r06/ab/summary.md.)
+        int least = 0, greatest = 0;
         hipStream_t st = nullptr;
-        if (hipExtStreamCreateWithCUMask(&st, uint32_t(mask.size()), mask.data()) != hipSuccess) {
+        if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess ||
+            hipStreamCreateWithPriority(&st, hipStreamNonBlocking, greatest) != hipSuccess) {
             (void)hipHostFree(h);
             break;
         }
@@ -1845,8 +1900,12 @@ ResidentReader* resident_reader(int device) {
 }
 
 // Whether the device's resident reader wave is on the GPU now (lock-free: the board's state word).
-std::atomic<ResidentReader*> g_resident_fast[64];
 bool resident_live(int device) {
+    static const int force = [] {  // PBF_SPARE_CU=0/1 forces the planning either way (A/B)
+        const char* e = std::getenv("PBF_SPARE_CU");
+        return e ? std::atoi(e) : -1;
+    }();
+    if (force >= 0) return force != 0;
     if (device < 0 || device >= 64) return false;
     ResidentReader* rr = g_resident_fast[device].load(std::memory_order_acquire);
     return rr && rr->host && __atomic_load_n(&rr->host->state, __ATOMIC_ACQUIRE) != 0;
@@ -2874,7 +2933,10 @@ int pbf_encode_data_blocks(int device, const uint8_t* keys, const uint64_t* key_
     HIP_TRY(allow_lds(k_encode_blocks, kEncodeLds));
     EncodeCtx& c = encode_ctx(device);
     std::lock_guard<std::mutex> lock(c.mu);
-    if (!c.stream) HIP_TRY(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
+    if (!c.stream) {
+        HIP_TRY(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
+        register_stream(device, c.stream);
+    }
     HIP_TRY(c.err.ensure(4));
     HIP_TRY(hipMemsetAsync(c.err.p, 0, 4, c.stream));
     const uint8_t *dk = keys, *dv = values;
@@ -3296,7 +3358,10 @@ int pbf_key_range_mask(int device, void* stream, const uint8_t* keys, const uint
     }
     EncodeCtx& c = encode_ctx(device);
     std::lock_guard<std::mutex> lock(c.mu);
-    if (!c.stream) HIP_TRY(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
+    if (!c.stream) {
+        HIP_TRY(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
+        register_stream(device, c.stream);
+    }
     hipStream_t s = on_device ? static_cast<hipStream_t>(stream) : c.stream;
     const uint8_t *dk = keys, *db = bounds;
     const uint64_t *dko = offsets, *dbo = bound_offsets;
