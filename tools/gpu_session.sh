@@ -111,6 +111,7 @@ for step in "$@"; do
     bench_c1_excl) PBF_SHARED_READERS=0 run bench_c1_excl 300 python bench.py --config c1 --steps 50 --warmup 5 ;;
     prof_c4_serial) PBF_STREAMS=1 prof prof_c4_serial 600 --config c4 --steps 2 --warmup 1 --no-cpu-baseline ;;
     ab_c3) ab abc3 300 1 --config c3 --steps 3 --warmup 1 ;;
+    ab_c3_2) ab abc3 300 2 --config c3 --steps 3 --warmup 1 ;;
     ab_c4) ab abc4 400 1 --config c4 --steps 3 --warmup 1 ;;
     ab_c5mixed) ab abc5m 300 1 --config c5mixed --steps 5 --warmup 2 ;;
     ab_c5) ab abc5 300 1 --config c5 --steps 5 --warmup 2 --no-host-c5 ;;
