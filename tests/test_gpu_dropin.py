@@ -412,3 +412,28 @@ def test_more_threads_than_resident_slots(oracle):
     for t in th:
         t.join(timeout=300)
     assert not errors, errors[:5]
+
+
+def test_partitions_planned_around_a_live_reader_in_a_subprocess(oracle):
+    """While the resident reader is live the tiled build / probe plan 31 partition workgroups per
+    XCD (groups_cap); PBF_SPARE_CU=1 forces that planning: builds equal the oracle and tiled probes
+    equal direct ones, for the ring (m = 2^30) and the counting-sort (variable-length) partitions."""
+    code = textwrap.dedent("""
+        import sys, numpy as np; sys.path.insert(0, '.')
+        from pebbledb_amd import BloomFilter, PackedKeys
+        from pebbledb_amd.keys import splitmix_hex_keys, varlen_keys
+        from oracle.oracle import COracle
+        o = COracle()
+        fx = PackedKeys.fixed(splitmix_hex_keys(61, 0, 3_000_000))
+        q = PackedKeys.fixed(splitmix_hex_keys(61, 1_500_000, 3_000_000))
+        d, off = varlen_keys(62, 0, 600_000)
+        vr = PackedKeys(d, 600_000, offsets=off)
+        for nb, k, keys, probes in ((2 ** 27, 6, fx, q), (3 * 2 ** 22 + 5, 8, vr, vr)):
+            bf = BloomFilter(nb, k); bf.set_build_mode(2); bf.add_many(keys)
+            assert bf.bitmap() == o.build(nb, k, keys, omp=True).tobytes(), nb
+            bf.set_probe_mode(2); t = bf.may_contain_many(probes, packed=True)
+            bf.set_probe_mode(1); dr = bf.may_contain_many(probes, packed=True)
+            assert np.array_equal(t, dr), nb
+        print('ok')
+    """)
+    assert _run_py(code, {"PBF_SPARE_CU": "1"}) == "ok"
