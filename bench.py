@@ -1318,6 +1318,13 @@ def main():
         events = events[:min(args.steps, 5)]
     build_ms = sum(e[0].elapsed_time(e[1]) for e in events) / len(events)
     probe_ms = sum(e[1].elapsed_time(e[2]) for e in events) / len(events)
+    # GPU time of a step (build + probe events) averaged over each quarter of the timed steps: shows
+    # whether the first steps of a short run are slower (clocks still ramping under sustained load)
+    quarters = None
+    if not args.no_events and len(events) >= 4:
+        per = [e[0].elapsed_time(e[2]) for e in events]
+        q = len(per) // 4
+        quarters = [round(sum(per[i * q:(i + 1) * q]) / q, 4) for i in range(4)]
     if world > 1:
         elapsed = float(all_reduce_scalar(torch, dist, elapsed, dist.ReduceOp.MAX, torch.float64))
         members_ok = bool(all_reduce_scalar(torch, dist, 1 if members_ok else 0, dist.ReduceOp.MIN, torch.int32))
@@ -1367,6 +1374,7 @@ def main():
                        "keys_per_step_per_gpu": 3 * n, "parallelism": f"filter-per-gpu x{world}"},
             "host_enqueue_ms_per_step": round((t_enq - t0) / args.steps * 1e3, 4),
             "gpu_span_ms_per_step": round(gpu_span_ms / args.steps, 4),
+            "gpu_ms_per_step_by_quarter": quarters,
             "host_wait_ms": {"stream_done": round((t_done - t_enq) * 1e3, 3), "device_sync": round((t1 - t_done) * 1e3, 3)},
             "build_ms": round(build_ms, 4),
             "probe_ms": round(probe_ms, 4),
