@@ -104,15 +104,148 @@ static PyObject* py_may_contain_set(PyObject* self, PyObject* const* args, Py_ss
     return Py_BuildValue("(iK)", 0, (unsigned long long)v);
 }
 
+/* candidates_one(key, level0, levels) -> the list lsm_get.candidates_one returns, or None when
+ * the Python path must take the call (a non-str key, a filter with buffered adds or another
+ * device, more than 64 filters, a comparison that raised, any library error: that path
+ * reproduces the reference's exceptions and raises the library's).  One LsmStorage.get(key)'s
+ * filter stage (reference src/lsm_storage.py:164-179): every L0 filter, newest first, then per
+ * level the tables with first_key <= key <= last_key (:173), all tested in ONE
+ * pbf_may_contain_set call; the result numbers the tables as candidate_masks rows. */
+static PyObject* s_fast, *s_first, *s_last, *s_bf;
+
+static int handle_of(PyObject* bf, void** out) { /* 1 ok, 0 fall back, -1 error */
+    PyObject* v = PyObject_GetAttr(bf, s_fast);
+    if (!v) {
+        PyErr_Clear();
+        return 0;
+    }
+    void* h = PyLong_Check(v) ? PyLong_AsVoidPtr(v) : NULL;
+    Py_DECREF(v);
+    if (!h) {
+        PyErr_Clear();
+        return 0;
+    }
+    *out = h;
+    return 1;
+}
+
+static PyObject* py_candidates_one(PyObject* self, PyObject* const* args, Py_ssize_t nargs) {
+    if (nargs != 3) {
+        PyErr_SetString(PyExc_TypeError, "candidates_one(key, level0, levels)");
+        return NULL;
+    }
+    if (!g_may_contain_set) {
+        PyErr_SetString(PyExc_RuntimeError, "_pebblefast is not bound to libpebblebloom.so");
+        return NULL;
+    }
+    PyObject* key = args[0];
+    if (!PyUnicode_Check(key)) Py_RETURN_NONE;
+    void* hs[64];
+    int32_t in_range[64];
+    uint32_t nt = 0, ni = 0;
+    PyObject* l0 = PySequence_Fast(args[1], "level0 must be a sequence");
+    if (!l0) {
+        PyErr_Clear();
+        Py_RETURN_NONE;
+    }
+    const Py_ssize_t n0 = PySequence_Fast_GET_SIZE(l0);
+    int ok = n0 <= 64;
+    for (Py_ssize_t i = 0; ok && i < n0; ++i) ok = handle_of(PySequence_Fast_GET_ITEM(l0, i), &hs[nt++]);
+    Py_DECREF(l0);
+    if (!ok) Py_RETURN_NONE;
+    PyObject* lv = PySequence_Fast(args[2], "levels must be a sequence");
+    if (!lv) {
+        PyErr_Clear();
+        Py_RETURN_NONE;
+    }
+    int32_t j = (int32_t)n0;
+    for (Py_ssize_t a = 0; ok && a < PySequence_Fast_GET_SIZE(lv); ++a) {
+        PyObject* lvl = PySequence_Fast(PySequence_Fast_GET_ITEM(lv, a), "a level must be a sequence");
+        if (!lvl) {
+            ok = 0;
+            break;
+        }
+        for (Py_ssize_t b = 0; ok && b < PySequence_Fast_GET_SIZE(lvl); ++b, ++j) {
+            PyObject* t = PySequence_Fast_GET_ITEM(lvl, b);
+            PyObject* first = PyObject_GetAttr(t, s_first);
+            PyObject* last = first ? PyObject_GetAttr(t, s_last) : NULL;
+            int in = -1;
+            if (last) {
+                in = PyObject_RichCompareBool(first, key, Py_LE);
+                if (in == 1) in = PyObject_RichCompareBool(key, last, Py_LE);
+            }
+            Py_XDECREF(first);
+            Py_XDECREF(last);
+            if (in < 0) {
+                ok = 0;
+                break;
+            }
+            if (!in) continue;
+            if (nt == 64) {
+                ok = 0;
+                break;
+            }
+            PyObject* bf = PyObject_GetAttr(t, s_bf);
+            ok = bf ? handle_of(bf, &hs[nt]) : 0;
+            Py_XDECREF(bf);
+            ++nt;
+            in_range[ni++] = j;
+        }
+        Py_DECREF(lvl);
+    }
+    Py_DECREF(lv);
+    if (!ok) {
+        PyErr_Clear();
+        Py_RETURN_NONE;
+    }
+    if (nt == 0) return PyList_New(0);
+    Py_ssize_t len;
+    const char* s = PyUnicode_AsUTF8AndSize(key, &len);
+    if (!s) {
+        PyErr_Clear();
+        Py_RETURN_NONE;
+    }
+    uint8_t bits[8] = {0};
+    int rc;
+    Py_BEGIN_ALLOW_THREADS
+    rc = g_may_contain_set(hs, nt, (const uint8_t*)s, (uint64_t)len, bits);
+    Py_END_ALLOW_THREADS
+    if (rc) Py_RETURN_NONE;
+    uint64_t v = 0;
+    for (int i = 0; i < 8; ++i) v |= (uint64_t)bits[i] << (8 * i);
+    PyObject* out = PyList_New(0);
+    if (!out) return NULL;
+    for (uint32_t i = 0; i < nt; ++i) {
+        if (!((v >> i) & 1u)) continue;
+        PyObject* x = PyLong_FromLong(i < (uint32_t)n0 ? (long)i : (long)in_range[i - (uint32_t)n0]);
+        if (!x || PyList_Append(out, x)) {
+            Py_XDECREF(x);
+            Py_DECREF(out);
+            return NULL;
+        }
+        Py_DECREF(x);
+    }
+    return out;
+}
+
 static PyMethodDef methods[] = {
     {"bind", py_bind, METH_VARARGS, "bind(pbf_may_contain address, pbf_may_contain_set address)"},
     {"may_contain", (PyCFunction)(void (*)(void))py_may_contain, METH_FASTCALL,
      "may_contain(handle, key) -> bool, or a negative result code"},
     {"may_contain_set", (PyCFunction)(void (*)(void))py_may_contain_set, METH_FASTCALL,
      "may_contain_set(handles, key) -> (rc, bits)"},
+    {"candidates_one", (PyCFunction)(void (*)(void))py_candidates_one, METH_FASTCALL,
+     "candidates_one(key, level0, levels) -> list of candidate rows, or None (take the Python path)"},
     {NULL, NULL, 0, NULL},
 };
 
 static struct PyModuleDef module = {PyModuleDef_HEAD_INIT, "_pebblefast", NULL, -1, methods};
 
-PyMODINIT_FUNC PyInit__pebblefast(void) { return PyModule_Create(&module); }
+PyMODINIT_FUNC PyInit__pebblefast(void) {
+    s_fast = PyUnicode_InternFromString("_fast");
+    s_first = PyUnicode_InternFromString("first_key");
+    s_last = PyUnicode_InternFromString("last_key");
+    s_bf = PyUnicode_InternFromString("bloom_filter");
+    if (!s_fast || !s_first || !s_last || !s_bf) return NULL;
+    return PyModule_Create(&module);
+}

@@ -355,7 +355,11 @@ struct pbf_filter {
     hipEvent_t wait_ev = nullptr;  // pbf_wait_stream: the caller's stream -> this stream
     hipEvent_t sig_ev = nullptr;   // pbf_signal_stream: this stream -> the caller's stream
     const char* last_kernel = "";  // the last kernel enqueued on the stream (wait_stream's report)
-    bool pending = false;          // work may be queued on the stream since its last completed wait
+    std::atomic<uint32_t> svc_id{0};  // index in the device reader's descriptor table (0: none yet)
+    // work may be queued on the stream since its last completed wait; set by writers (lock held
+    // exclusively), cleared by a wait or by a reader whose stream query found the stream drained
+    // (lock held shared: concurrent readers may clear it together, hence atomic)
+    std::atomic<bool> pending{false};
     // Writers (builds, from_bytes, batch probes: anything that touches the handle's state or
     // queues work on its stream) hold it exclusively; one-key probes of a built filter hold it
     // shared and run on a reader stream, so concurrent readers do not queue behind each other
@@ -1795,6 +1799,12 @@ struct ResidentReader {
     std::vector<uint32_t> free_slots;
     uint64_t idle_ticks = 0, life_ticks = 0;
     int device = 0;
+    // the board's descriptor table (reader_service.hpp SvcBoard::desc): indexes handed to filters
+    // at their first resident probe, returned when they are destroyed; every return bumps the
+    // epoch, which requests carry, so the wave's descriptor cache never outlives an index's owner
+    std::vector<uint32_t> free_ids;
+    uint32_t next_id = 1;
+    std::atomic<uint32_t> epoch{1};
 };
 
 std::atomic<int> g_resident_on{-1};  // -1: PBF_RESIDENT_READER not read yet
@@ -1946,11 +1956,45 @@ struct ResidentSlot {
     }
 };
 
+// f's index in rr's descriptor table, registering it (its descriptor written to the board) on
+// first use; 0 when the table is full (the caller launches per key).
+uint32_t svc_index(ResidentReader* rr, pbf_filter_t* f) {
+    uint32_t id = f->svc_id.load(std::memory_order_acquire);
+    if (id) return id;
+    std::lock_guard<std::mutex> lock(rr->mu);
+    id = f->svc_id.load(std::memory_order_relaxed);
+    if (id) return id;
+    if (!rr->free_ids.empty()) {
+        id = rr->free_ids.back();
+        rr->free_ids.pop_back();
+    } else if (rr->next_id < kSvcDescs) {
+        id = rr->next_id++;
+    } else {
+        return 0;
+    }
+    rr->host->desc[id] = SvcFilter{f->bitmap, f->im};  // before any request names id (x86: in order)
+    f->svc_id.store(id, std::memory_order_release);
+    return id;
+}
+
+// pbf_destroy: f's index back to its device's table.  The epoch moves on, so a request that names
+// the index for its next owner cannot meet f's descriptor in the wave's cache.
+void svc_release(pbf_filter_t* f) {
+    const uint32_t id = f->svc_id.load(std::memory_order_acquire);
+    if (!id || f->device < 0 || f->device >= 64) return;
+    ResidentReader* rr = g_resident_fast[f->device].load(std::memory_order_acquire);
+    if (!rr) return;
+    std::lock_guard<std::mutex> lock(rr->mu);
+    rr->epoch.fetch_add(1, std::memory_order_acq_rel);
+    rr->free_ids.push_back(id);
+    f->svc_id.store(0, std::memory_order_relaxed);
+}
+
 // One key against nf filters sharing k through the resident reader: *bits (bit f = filters f's
 // answer) and *taken = true, or *taken = false when this call cannot use it (disabled, key or
-// set too large, no free slot, no board): the caller launches per key.  The filters' bitmaps
-// must have no work still queued (reader_ok).
-int resident_probe(int device, const SvcFilter* fs, uint32_t nf, uint32_t k, const uint8_t* key, uint64_t len,
+// set too large, no free slot, no board, descriptor table full): the caller launches per key.
+// The filters' bitmaps must have no work still queued (reader_ok).
+int resident_probe(int device, pbf_filter_t* const* fs, uint32_t nf, uint32_t k, const uint8_t* key, uint64_t len,
                    uint64_t* bits, bool* taken) {
     *taken = false;
     if (!resident_enabled() || len > kSvcKeyMax || k == 0 || k > 32 || nf == 0 || nf > kSvcFilters) return PBF_OK;
@@ -1975,12 +2019,19 @@ int resident_probe(int device, const SvcFilter* fs, uint32_t nf, uint32_t k, con
         ts.seq = __atomic_load_n(&rr->host->head[slot].req, __ATOMIC_ACQUIRE);  // a recycled slot's last
     }
     ResidentReader* rr = ts.rr;
+    uint16_t ids[kSvcFilters];
+    for (uint32_t i = 0; i < nf; ++i) {
+        const uint32_t id = svc_index(rr, fs[i]);
+        if (!id) return PBF_OK;
+        ids[i] = uint16_t(id);
+    }
+    const uint32_t epoch = rr->epoch.load(std::memory_order_acquire);  // (after the registrations)
     SvcHead& hd = rr->host->head[ts.slot];
     SvcSlot& sl = rr->host->slot[ts.slot];
-    // the body first (filters past the first, a key too long for the head), then head line 1
-    // (its tag req2 last), then line 0 (req last): the wave takes the request once both lines
-    // carry the new sequence (reader_service.hpp SvcHead)
-    if (nf > 1) std::memcpy(sl.f + 1, fs + 1, size_t(nf - 1) * sizeof(SvcFilter));
+    // the body first (indexes past the 16th, a key too long for the head), then head line 1 (its
+    // tag req2 last), then line 0 (req last): the wave takes the request once both lines carry the
+    // new sequence (reader_service.hpp SvcHead)
+    if (nf > kSvcInlineIds) std::memcpy(sl.ids + kSvcInlineIds, ids + kSvcInlineIds, (nf - kSvcInlineIds) * sizeof(uint16_t));
     const bool inl = len <= kSvcInlineKey;
     if (!inl) std::memcpy(sl.key, key, len);
     uint32_t seq = ts.seq + 1;
@@ -1988,10 +2039,9 @@ int resident_probe(int device, const SvcFilter* fs, uint32_t nf, uint32_t k, con
     ts.seq = seq;
     if (inl && len > 16) std::memcpy(hd.key1, key + 16, len - 16);
     __atomic_store_n(&hd.req2, seq, __ATOMIC_RELEASE);
-    hd.nf = nf;
-    hd.len = uint32_t(len);
-    hd.k = k;
-    hd.f0 = fs[0];
+    hd.shape = nf | (k << 8) | (uint32_t(len) << 16);
+    hd.epoch = epoch;
+    std::memcpy(hd.ids, ids, std::min(nf, kSvcInlineIds) * sizeof(uint16_t));
     if (inl && len) std::memcpy(hd.key0, key, std::min<uint64_t>(len, 16));
     __atomic_store_n(&hd.req, seq, __ATOMIC_RELEASE);
     int rc = PBF_OK;
@@ -2013,7 +2063,7 @@ int resident_probe(int device, const SvcFilter* fs, uint32_t nf, uint32_t k, con
                 // Retract the request before the caller may free or rebuild the bitmap: a wave
                 // that has not taken it yet acknowledges a head with no filters without reading
                 // any memory; one that has taken it answers within microseconds of doing so.
-                __atomic_store_n(&hd.nf, 0u, __ATOMIC_RELEASE);
+                __atomic_store_n(&hd.shape, 0u, __ATOMIC_RELEASE);
                 const auto t1 = std::chrono::steady_clock::now();
                 while (__atomic_load_n(&sl.ack, __ATOMIC_ACQUIRE) != seq &&
                        __atomic_load_n(&rr->host->state, __ATOMIC_ACQUIRE) != 0 &&
@@ -2040,25 +2090,31 @@ bool reader_ok(pbf_filter_t* f, uint64_t len) {
     if (!enabled) return false;
     if (f->k == 0) return true;
     if (kmax_for(f->k) == 0 || len > kOneKeyMax || f->pristine) return false;
-    if (!f->pending) return true;
+    if (!f->pending.load(std::memory_order_relaxed)) return true;
     const hipError_t q = hipStreamQuery(f->stream);
-    if (q != hipSuccess) (void)hipGetLastError();
-    return q == hipSuccess;
+    if (q != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    // drained: later readers skip the query (a get probes the same published filters again and
+    // again; 16 stream queries cost a get several microseconds).  No writer can have queued work
+    // since: writers hold the lock exclusively and this reader holds it shared.
+    f->pending.store(false, std::memory_order_relaxed);
+    return true;
 }
 
 // One key of a built filter (reader_ok, lock held shared) through the resident reader:
 // PBF_OK with *out, an error, or kNotTaken when the reader does not take it (the caller launches).
 constexpr int kNotTaken = 1;
 int one_key_resident(pbf_filter_t* f, const uint8_t* key, uint64_t len, int* out) {
-    SvcFilter sf{f->bitmap, f->im};
     uint64_t bits = 0;
     bool taken = false;
-    const int rc = resident_probe(f->device, &sf, 1, f->k, key, len, &bits, &taken);
+    const int rc = resident_probe(f->device, &f, 1, f->k, key, len, &bits, &taken);
     if (rc) return rc;
     if (!taken) return kNotTaken;
     *out = int(bits & 1u);
-    f->last_probe_mode = PBF_PROBE_DIRECT;
-    f->last_probe_detail = PBF_DETAIL_ONE_KEY | PBF_DETAIL_SHARED | PBF_DETAIL_RESIDENT;
+    f->last_probe_mode.store(PBF_PROBE_DIRECT, std::memory_order_relaxed);
+    f->last_probe_detail.store(PBF_DETAIL_ONE_KEY | PBF_DETAIL_SHARED | PBF_DETAIL_RESIDENT, std::memory_order_relaxed);
     return PBF_OK;
 }
 
@@ -2207,11 +2263,11 @@ int may_contain_set_locked(pbf_filter_t* const* fs, uint32_t nf, const uint8_t* 
         for (size_t c0 = 0; c0 < idx.size(); c0 += kMaxFilterSet) {
             const uint32_t nsub = uint32_t(std::min<size_t>(kMaxFilterSet, idx.size() - c0));
             if (shared) {  // every handle reader_ok: the resident reader may answer
-                SvcFilter sf[kMaxFilterSet];
-                for (uint32_t j = 0; j < nsub; ++j) sf[j] = SvcFilter{fs[idx[c0 + j]]->bitmap, fs[idx[c0 + j]]->im};
+                pbf_filter_t* sub[kMaxFilterSet];
+                for (uint32_t j = 0; j < nsub; ++j) sub[j] = fs[idx[c0 + j]];
                 uint64_t bits = 0;
                 bool taken = false;
-                rc = resident_probe(f0->device, sf, nsub, k, key, len, &bits, &taken);
+                rc = resident_probe(f0->device, sub, nsub, k, key, len, &bits, &taken);
                 if (rc) return rc;
                 if (taken) {
                     for (uint32_t j = 0; j < nsub; ++j) {
@@ -2442,6 +2498,7 @@ int pbf_destroy(pbf_filter_t* f) {
     // streams are never destroyed, so a later lease from another stream still waits on the
     // set's event.)
     if (f->stream) (void)hipStreamSynchronize(f->stream);
+    svc_release(f);  // (no request names f any more: its callers have returned)
     if (f->bitmap) bitmap_release(f->device, bitmap_alloc_bytes(f->alloc_words), f->bitmap);
     if (f->ev) (void)hipEventDestroy(f->ev);
     if (f->wait_ev) (void)hipEventDestroy(f->wait_ev);
@@ -2840,6 +2897,47 @@ int pbf_may_contain_set(pbf_filter_t* const* filters, uint32_t nfilters, const u
         if (!filters[i]) return fail(PBF_ERR_INVALID, "null filter handle in set");
         if (filters[i]->device != filters[0]->device) return fail(PBF_ERR_INVALID, "filters of one set must share a device");
     }
+    if (nfilters <= kSvcFilters) {
+        // LsmStorage.get's usual set (product-sized filters of one k, at most 64): straight to the
+        // resident reader with no allocation -- the distinct handles in address order on the stack,
+        // held shared while the reader answers
+        pbf_filter_t* ord[kSvcFilters];
+        std::copy(filters, filters + nfilters, ord);
+        std::sort(ord, ord + nfilters);
+        const uint32_t nu = uint32_t(std::unique(ord, ord + nfilters) - ord);
+        struct Held {
+            pbf_filter_t** p;
+            uint32_t n = 0;
+            ~Held() {
+                for (uint32_t i = 0; i < n; ++i) p[i]->mu.unlock_shared();
+            }
+        } held{ord};
+        const uint32_t k0 = filters[0]->k;
+        bool ok = k0 > 0 && kmax_for(k0) > 0;
+        for (uint32_t i = 0; i < nu && ok; ++i) {
+            ord[i]->mu.lock_shared();
+            held.n = i + 1;
+            ok = ord[i]->k == k0 && reader_ok(ord[i], len);
+        }
+        if (ok) {
+            uint64_t bits = 0;
+            bool taken = false;
+            const int rc = resident_probe(filters[0]->device, filters, nfilters, k0, key, len, &bits, &taken);
+            if (rc) return rc;
+            if (taken) {
+                std::memset(out_bits, 0, (nfilters + 7) / 8);
+                for (uint32_t i = 0; i < nfilters; ++i)
+                    if ((bits >> i) & 1u) out_bits[i >> 3] |= uint8_t(1u << (i & 7));
+                for (uint32_t i = 0; i < nu; ++i) {
+                    ord[i]->last_probe_mode.store(PBF_PROBE_DIRECT, std::memory_order_relaxed);
+                    ord[i]->last_probe_detail.store(PBF_DETAIL_ONE_KEY | PBF_DETAIL_SET | PBF_DETAIL_RESIDENT,
+                                                    std::memory_order_relaxed);
+                }
+                return PBF_OK;
+            }
+        }
+        // otherwise (locks released here): the general path below
+    }
     // every distinct handle of the set, in address order (a table may appear twice)
     std::vector<pbf_filter_t*> order(filters, filters + nfilters);
     std::sort(order.begin(), order.end());
@@ -2863,11 +2961,9 @@ int pbf_may_contain_set(pbf_filter_t* const* filters, uint32_t nfilters, const u
             bool one_k = nfilters <= kSvcFilters && k0 > 0 && kmax_for(k0) > 0;
             for (uint32_t i = 1; i < nfilters && one_k; ++i) one_k = filters[i]->k == k0;
             if (one_k) {
-                SvcFilter sf[kSvcFilters];
-                for (uint32_t i = 0; i < nfilters; ++i) sf[i] = SvcFilter{filters[i]->bitmap, filters[i]->im};
                 uint64_t bits = 0;
                 bool taken = false;
-                const int rc = resident_probe(filters[0]->device, sf, nfilters, k0, key, len, &bits, &taken);
+                const int rc = resident_probe(filters[0]->device, filters, nfilters, k0, key, len, &bits, &taken);
                 if (rc) return rc;
                 if (taken) {
                     std::memset(out_bits, 0, (nfilters + 7) / 8);

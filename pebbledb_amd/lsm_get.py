@@ -30,6 +30,7 @@ from typing import NamedTuple, Sequence
 import numpy as np
 
 from . import _native
+from . import bloom_filter as _bfm
 from .bloom_filter import BloomFilter, _default_device, may_contain_multi, may_contain_set_bits
 from .keys import PackedKeys
 
@@ -103,7 +104,13 @@ def candidates_one(key: str, level0: Sequence[BloomFilter], levels: Sequence[Seq
     """The SSTables ``LsmStorage.get(key)`` would read if none held the key, in its order
     (lsm_storage.py:164-179), numbered as ``candidate_masks`` rows: L0 filters (newest first)
     and the level filters whose ``first_key <= key <= last_key`` (:173) are tested together in
-    one ``pbf_may_contain_set`` launch."""
+    one ``pbf_may_contain_set`` launch.  The whole stage runs in C (``_pebblefast.candidates_one``:
+    the range checks, the handles and the call, ~3 us less per get than this loop); it hands back
+    None when this path must take the call (buffered adds, a non-str key, filters on several
+    devices, more than 64 filters), which then raises what the reference raises."""
+    r = (_bfm._FAST or _bfm._fast()).candidates_one(key, level0, levels)
+    if r is not None:
+        return r
     n0 = len(level0)
     in_range, tested = [], list(level0)
     j = n0

@@ -1,0 +1,55 @@
+"""Which path one get's filter stage takes (lsm_get.candidates_one: the C stage or the Python
+loop) and what each costs, on the bench's 16-filter set (bench.py get_set_latency)."""
+import sys
+import time
+
+sys.path.insert(0, ".")
+from pebbledb_amd import BloomFilter, bloom_filter  # noqa: E402
+from pebbledb_amd.keys import splitmix_hex_keys_str  # noqa: E402
+from pebbledb_amd.lsm_get import LevelTable, candidates_one, may_contain_set_bits  # noqa: E402
+
+SEED = 0x5EEDB100
+ns = [20_000 + 10_000 * i for i in range(16)]
+tables, start = [], 0
+for n in ns:
+    keys = sorted(splitmix_hex_keys_str(SEED, start, n))
+    tables.append((keys[0], keys[-1], BloomFilter.build_from_keys_and_fp_rate(keys, 0.001, device=0)))
+    start += n
+l0 = [bf for _, _, bf in tables[:10]]
+levels = [[LevelTable("", "\U0010ffff", bf) for _, _, bf in tables[10:]]]
+flat = l0 + [t.bloom_filter for t in levels[0]]
+probes = splitmix_hex_keys_str(SEED, start - 500, 1000)
+fast = bloom_filter._FAST or bloom_filter._fast()
+print("fast handles:", [bf._fast != 0 for bf in flat])
+print("C stage result:", fast.candidates_one(probes[0], l0, levels), "python:", candidates_one(probes[0], l0, levels))
+import ctypes  # noqa: E402
+from pebbledb_amd import _native  # noqa: E402
+L = _native.lib()
+hs16 = (ctypes.c_void_p * 16)(*[bf._fast for bf in flat])
+hs1 = (ctypes.c_void_p * 1)(flat[-1]._fast)
+bits = (ctypes.c_uint8 * 8)()
+tup16 = tuple(bf._fast for bf in flat)
+enc = [p.encode() for p in probes]
+for name, fn in (("ctypes set 16", lambda k: L.pbf_may_contain_set(hs16, 16, k.encode(), len(k), bits)),
+                 ("ctypes set 1", lambda k: L.pbf_may_contain_set(hs1, 1, k.encode(), len(k), bits)),
+                 ("fast.may_contain_set 1", lambda k: fast.may_contain_set((flat[-1]._fast,), k)),
+                 ("fast.may_contain_set tuple16", lambda k: fast.may_contain_set(tup16, k)),
+                 ("fast.may_contain 1", lambda k: fast.may_contain(flat[-1]._fast, k)),
+                 ("C stage", lambda k: fast.candidates_one(k, l0, levels)),
+                 ("candidates_one", lambda k: candidates_one(k, l0, levels)),
+                 ("may_contain_set_bits", lambda k: may_contain_set_bits(flat, k)),
+                 ("fast.may_contain_set", lambda k: fast.may_contain_set([bf._fast for bf in flat], k))):
+    for _ in range(200):
+        fn(probes[_ % 1000])
+    t = time.perf_counter()
+    for i in range(5000):
+        fn(probes[i % 1000])
+    print("%-22s %.2f us" % (name, (time.perf_counter() - t) / 5000 * 1e6))
+
+# the same library call loop in C, inside this process, over these filters
+lib = ctypes.CDLL("tools/microbench/get_latency.so")
+lib.loop_set.restype = ctypes.c_double
+lib.loop_set.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_int, ctypes.c_int]
+kb = b"".join(enc)
+print("C loop in-process, 16: %.2f us" % lib.loop_set(hs16, 16, kb, 1000, 20000))
+print("C loop in-process, 1:  %.2f us" % lib.loop_set(hs1, 1, kb, 1000, 20000))

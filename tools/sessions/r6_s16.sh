@@ -1,0 +1,9 @@
+#!/bin/bash
+# Round 6 session 16: which path a get's filter stage takes, and its cost by layer, beside the
+# C-level latencies on the same box.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+mkdir -p gpurun_out
+timeout -k 10 120 tools/microbench/get_latency 20000 > gpurun_out/s16_getlat.log 2>&1 || { cat gpurun_out/s16_getlat.log; exit 1; }
+cat gpurun_out/s16_getlat.log
+timeout -k 10 300 python3 tools/diag/get_stage_check.py > gpurun_out/s16.log 2>&1 || { cat gpurun_out/s16.log; exit 1; }
+cat gpurun_out/s16.log
