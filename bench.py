@@ -20,6 +20,7 @@ Rank 0 prints one JSON line.
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -279,11 +280,13 @@ def dropin_latency(device, reps=2000):
         t_add = time.perf_counter() - t0
         for k in probes[:50]:
             bf.may_contain(k)
+        st0 = _resident_stats(device) if cls is BloomFilter else None
         t0 = time.perf_counter()
         hits = 0
         for i in range(reps):
             hits += bf.may_contain(probes[i % 1000])
         t_mc = time.perf_counter() - t0
+        st1 = _resident_stats(device) if cls is BloomFilter else None
         t0 = time.perf_counter()
         for _ in range(200):
             blob = bf.to_bytes()
@@ -297,6 +300,8 @@ def dropin_latency(device, reps=2000):
                      "hits": hits, "bitmap_sha16": __import__("hashlib").sha256(blob).hexdigest()[:16]}
         if cls is BloomFilter:
             out[name]["build_from_keys_1k_us"] = round(t_bk / 20 * 1e6, 1)
+            # of the call's time, the resident wave's own (request seen -> answer written)
+            out[name]["may_contain_device_us"] = round((st1[1] - st0[1]) * 1e-3 / max(1, st1[0] - st0[0]), 2)
             # where the per-key time goes: the same calls with a launch per key (the resident
             # reader off)
             L = _native_lib()
@@ -387,6 +392,13 @@ def _native_lib():
     return _native.lib()
 
 
+def _resident_stats(device):
+    """(requests answered, their device nanoseconds) of the device's resident reader so far."""
+    r, d = ctypes.c_uint64(), ctypes.c_uint64()
+    _native_lib().pbf_resident_stats(device, ctypes.byref(r), ctypes.byref(d))
+    return r.value, d.value
+
+
 def get_set_latency(device, reps=1000):
     """One LsmStorage.get's bloom checks (src/lsm_storage.py:164-179) over 10 L0 + 6 level SSTable
     filters of 16 different sizes (product sizing, sstable.py:274: 20k..170k keys, k = 10): one
@@ -407,9 +419,11 @@ def get_set_latency(device, reps=1000):
     probes = splitmix_hex_keys_str(SEED, start - 500, 1000)  # 500 members of the last table, 500 absent
     for key in probes[:50]:
         candidates_one(key, l0, levels)
+    st0 = _resident_stats(device)
     t0 = time.perf_counter()
     one = [candidates_one(probes[i % 1000], l0, levels) for i in range(reps)]
     t_set = time.perf_counter() - t0
+    st1 = _resident_stats(device)
     t0 = time.perf_counter()
     loop = [[t for t, bf in enumerate(flat) if bf.may_contain(probes[i % 1000])] for i in range(reps)]
     t_loop = time.perf_counter() - t0
@@ -425,6 +439,7 @@ def get_set_latency(device, reps=1000):
         L.pbf_resident_enable(1)
     return {"filters": len(flat), "nb_bytes": [bf.nb_bytes for bf in flat],
             "one_call_us_per_get": round(t_set / reps * 1e6, 2),
+            "one_call_device_us": round((st1[1] - st0[1]) * 1e-3 / max(1, st1[0] - st0[0]), 2),
             "one_launch_us_per_get": round(t_launch / reps * 1e6, 2),
             "may_contain_x16_us_per_get": round(t_loop / reps * 1e6, 2),
             "identical": one == loop == launched}

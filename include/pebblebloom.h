@@ -159,6 +159,10 @@ int pbf_may_contain_set(pbf_filter_t* const* filters, uint32_t nfilters, const u
  * threads beyond 64 per device take the per-key launch.  *launches = the waves started so far on
  * `device` (0 before the first resident answer). */
 int pbf_resident_launches(int device, uint32_t* launches);
+/* Requests the device's resident reader has answered so far, and the wave's time on them: from
+ * seeing a request in its poll to writing the answer (device wall clock), summed.  The rest of a
+ * call's time is the host's and the bus's (posting, the poll's round trip, the answer's write). */
+int pbf_resident_stats(int device, uint64_t* requests, uint64_t* device_ns);
 /* Turns the resident reader on (1) or off (0) for later calls of the process (overrides
  * PBF_RESIDENT_READER; a wave already resident leaves after its idle time). */
 int pbf_resident_enable(int on);

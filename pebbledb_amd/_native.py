@@ -42,6 +42,7 @@ SIGNATURES = {
     "pbf_build": (_int, [_vp, _u8p, _vp, _u64, _int]),
     "pbf_murmur3_x86_32": (_int, [_int, ctypes.c_char_p, _u64, _u32, ctypes.POINTER(ctypes.c_int32)]),
     "pbf_resident_launches": (_int, [_int, ctypes.POINTER(_u32)]),
+    "pbf_resident_stats": (_int, [_int, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
     "pbf_resident_enable": (_int, [_int]),
     "pbf_probe_fixed": (_int, [_vp, _u8p, _u32, _u64, _u8p, _int]),
     "pbf_probe": (_int, [_vp, _u8p, _vp, _u64, _u8p, _int]),

@@ -329,24 +329,39 @@ size_t max_scratch_sets() {
 
 }  // namespace
 
-struct pbf_filter {
+struct alignas(128) pbf_filter {
+    // The fields a per-key probe reads (or writes) of every filter it tests, together in the first
+    // 128 bytes: a get over 16 filters from Python otherwise paid ~0.1 us per filter in cache
+    // misses on four lines of each (tools/diag/get_stage_check.py).
+    //
+    // Writers (builds, from_bytes, batch probes: anything that touches the handle's state or
+    // queues work on its stream) hold mu exclusively; one-key probes of a built filter hold it
+    // shared and run on a reader stream, so concurrent readers do not queue behind each other
+    // (the reference's get probes a published filter from any thread, lsm_storage.py:153-179).
+    std::shared_mutex mu;
     int device = 0;
+    uint32_t k = 0;
+    std::atomic<uint32_t> svc_id{0};  // index in the device reader's descriptor table (0: none yet)
+    // work may be queued on the stream since its last completed wait; set by writers (lock held
+    // exclusively), cleared by a wait or by a reader whose stream query found the stream drained
+    // (lock held shared: concurrent readers may clear it together, hence atomic)
+    std::atomic<bool> pending{false};
+    bool pristine = true;  // logically all-zero; reachable words not yet materialised
+    std::atomic<int> last_probe_mode{0};          // (written by concurrent readers too)
+    std::atomic<uint32_t> last_probe_detail{0};   // PBF_DETAIL_* of the last probe
+    uint32_t* bitmap = nullptr;
+    IndexMap im{};
+    // the rest
     hipStream_t stream = nullptr;
     uint64_t nb_bytes = 0;
-    uint32_t k = 0;
     uint64_t words = 0;  // logical words ceil(nb_bytes / 4)
     uint64_t alloc_words = 0;
-    uint32_t* bitmap = nullptr;
-    bool pristine = true;  // logically all-zero; reachable words not yet materialised
     bool middle_dirty = false;  // m > 2^32: unreachable middle written by set_bitmap
     int mode = PBF_BUILD_AUTO;
     int last_mode = 0;
-    IndexMap im{};
     TileMap tm{};
     bool tiled_ok = false;
     int probe_mode = PBF_PROBE_AUTO;
-    std::atomic<int> last_probe_mode{0};          // (written by concurrent readers too)
-    std::atomic<uint32_t> last_probe_detail{0};   // PBF_DETAIL_* of the last probe
     uint32_t last_build_detail = 0;  // PBF_DETAIL_* | (kps / 256) << 12 of the last tiled build
     Scratch* sc = nullptr;           // leased for the current call
     bool spare_cu = false;           // the current tiled call plans around a resident reader (groups_cap)
@@ -355,17 +370,8 @@ struct pbf_filter {
     hipEvent_t wait_ev = nullptr;  // pbf_wait_stream: the caller's stream -> this stream
     hipEvent_t sig_ev = nullptr;   // pbf_signal_stream: this stream -> the caller's stream
     const char* last_kernel = "";  // the last kernel enqueued on the stream (wait_stream's report)
-    std::atomic<uint32_t> svc_id{0};  // index in the device reader's descriptor table (0: none yet)
-    // work may be queued on the stream since its last completed wait; set by writers (lock held
-    // exclusively), cleared by a wait or by a reader whose stream query found the stream drained
-    // (lock held shared: concurrent readers may clear it together, hence atomic)
-    std::atomic<bool> pending{false};
-    // Writers (builds, from_bytes, batch probes: anything that touches the handle's state or
-    // queues work on its stream) hold it exclusively; one-key probes of a built filter hold it
-    // shared and run on a reader stream, so concurrent readers do not queue behind each other
-    // (the reference's get probes a published filter from any thread, lsm_storage.py:153-179).
-    std::shared_mutex mu;
 };
+static_assert(offsetof(pbf_filter, im) + sizeof(IndexMap) <= 128, "per-key fields in the first 128 bytes");
 
 namespace {
 
@@ -1805,6 +1811,9 @@ struct ResidentReader {
     std::vector<uint32_t> free_ids;
     uint32_t next_id = 1;
     std::atomic<uint32_t> epoch{1};
+    // answered requests and the wave's time on them (pbf_resident_stats)
+    std::atomic<uint64_t> answered{0}, answer_ticks{0};
+    uint64_t khz = 0;
 };
 
 std::atomic<int> g_resident_on{-1};  // -1: PBF_RESIDENT_READER not read yet
@@ -1897,6 +1906,7 @@ ResidentReader* resident_reader(int device) {
         rr->stream = st;
         rr->done = ev;
         rr->device = device;
+        rr->khz = uint64_t(khz);
         const char* e = std::getenv("PBF_RESIDENT_IDLE_US");
         const uint64_t idle_us = e && std::atoi(e) > 0 ? uint64_t(std::atoi(e)) : 2000;
         rr->idle_ticks = uint64_t(khz) * idle_us / 1000;
@@ -2074,6 +2084,8 @@ int resident_probe(int device, pbf_filter_t* const* fs, uint32_t nf, uint32_t k,
         }
     }
     *bits = __atomic_load_n(&sl.bits, __ATOMIC_ACQUIRE);
+    rr->answered.fetch_add(1, std::memory_order_relaxed);
+    rr->answer_ticks.fetch_add(__atomic_load_n(&sl.ticks, __ATOMIC_RELAXED), std::memory_order_relaxed);
     *taken = true;
     return PBF_OK;
 }
@@ -2827,6 +2839,17 @@ int pbf_signal_stream(pbf_filter_t* f, void* stream) {
 
 int pbf_resident_enable(int on) {
     g_resident_on.store(on ? 1 : 0);
+    return PBF_OK;
+}
+
+int pbf_resident_stats(int device, uint64_t* requests, uint64_t* device_ns) {
+    if (!requests || !device_ns) return fail(PBF_ERR_INVALID, "null out");
+    *requests = *device_ns = 0;
+    ResidentReader* rr = device >= 0 && device < 64 ? g_resident_fast[device].load(std::memory_order_acquire) : nullptr;
+    if (rr && rr->khz) {
+        *requests = rr->answered.load(std::memory_order_relaxed);
+        *device_ns = rr->answer_ticks.load(std::memory_order_relaxed) * 1000000ull / rr->khz;
+    }
     return PBF_OK;
 }
 

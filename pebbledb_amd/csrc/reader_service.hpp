@@ -68,7 +68,7 @@ static_assert(sizeof(SvcHead) == 128, "SvcHead layout: two lines");
 
 struct SvcSlot {
     uint32_t ack;      // device: the sequence answered, stored with `bits`
-    uint32_t pad0;
+    uint32_t ticks;    // device: wall-clock ticks from seeing the request to answering it
     uint64_t bits;     // device: bit f = filters[f] may contain the key
     uint8_t pad1[48];  // the body starts on its own 64-B line
     uint16_t ids[kSvcFilters];            // indexes of filters [16, nf)
@@ -114,8 +114,10 @@ __device__ __forceinline__ uint4 svc_touch(svc_v4u v) {
 // compiles to an L2 write-back (buffer_wbl2) of this XCD's whole L2 per answer: with ~200k gets/s
 // that slowed a concurrent batched probe by 40% (profiles/r06/s3).  The board is coherent host
 // memory, which the GPU does not cache.
-__device__ __forceinline__ void svc_ack(SvcSlot* sl, uint32_t req, uint64_t bits) {
-    const svc_v4u x = {req, 0u, uint32_t(bits), uint32_t(bits >> 32)};
+// (The second word carries the wall-clock ticks from the request's detection to the answer: the
+// host's pbf_resident_stats.)
+__device__ __forceinline__ void svc_ack(SvcSlot* sl, uint32_t req, uint64_t bits, uint32_t ticks) {
+    const svc_v4u x = {req, ticks, uint32_t(bits), uint32_t(bits >> 32)};
     *reinterpret_cast<volatile svc_v4u*>(sl) = x;
 }
 
@@ -132,7 +134,7 @@ struct SvcLds {
 
 // One request of slot s, its head lines in LDS (hb, 32 words).
 __device__ __forceinline__ void svc_answer(SvcBoard* b, uint32_t s, uint32_t req, uint32_t nf, uint32_t len, uint32_t k,
-                                           SvcLds& L) {
+                                           SvcLds& L, uint64_t t_seen) {
     const uint32_t lane = threadIdx.x;
     SvcSlot* sl = b->slot + s;
     // the key and the filters' indexes: from the head, or (a longer key, filters past 16) the body
@@ -222,7 +224,7 @@ __device__ __forceinline__ void svc_answer(SvcBoard* b, uint32_t s, uint32_t req
     __syncthreads();
     const bool hit = lane < nf && L.miss[lane] == 0u;
     const unsigned long long bal = __ballot(hit);
-    if (lane == 0) svc_ack(sl, req, uint64_t(bal));
+    if (lane == 0) svc_ack(sl, req, uint64_t(bal), uint32_t(wall_clock64() - t_seen));
     __syncthreads();  // kw, hb, rq and miss are rewritten by the next request
 }
 
@@ -274,6 +276,7 @@ __global__ void __launch_bounds__(64) k_reader_service(SvcBoard* b, uint32_t id,
             while (pend) {
                 const uint32_t g = uint32_t(__builtin_ctzll(pend)) >> 3;
                 pend &= pend - 1;
+                const uint64_t t_seen = wall_clock64();
                 if (grp == g) reinterpret_cast<uint4*>(L.hb)[piece] = hv[i];
                 __syncthreads();
                 const uint32_t rq = L.hb[0], shape = L.hb[1], epoch = L.hb[2];
@@ -287,9 +290,9 @@ __global__ void __launch_bounds__(64) k_reader_service(SvcBoard* b, uint32_t id,
                         cepoch = epoch;
                         __syncthreads();
                     }
-                    svc_answer(b, s, rq, nf, len, k, L);
+                    svc_answer(b, s, rq, nf, len, k, L, t_seen);
                 } else {
-                    if (lane == 0) svc_ack(b->slot + s, rq, 0);
+                    if (lane == 0) svc_ack(b->slot + s, rq, 0, 0);
                     __syncthreads();
                 }
                 if (grp == g) done[i] = rq;

@@ -437,3 +437,54 @@ def test_partitions_planned_around_a_live_reader_in_a_subprocess(oracle):
         print('ok')
     """)
     assert _run_py(code, {"PBF_SPARE_CU": "1"}) == "ok"
+
+
+def test_resident_descriptor_indexes_cached_and_reused(oracle):
+    """The resident reader names filters by descriptor-table index and caches their descriptors
+    in LDS (reader_service.hpp): 300 filters of different sizes (more than the 256 cache entries,
+    so indexes collide), gets over sets of 64 (indexes past the 16th travel in the slot body), then
+    100 filters destroyed and 100 new ones of OTHER sizes built, which take the freed indexes: the
+    epoch must keep the cache from answering with a destroyed filter's descriptor.  Every answer
+    equals the oracle's."""
+    import gc
+    from pebbledb_amd import may_contain_set
+    k = 7
+
+    def make(i, gen):
+        nb = 211 + 37 * i + 1009 * gen  # every filter a different m, and a new one per generation
+        members = PackedKeys.fixed(splitmix_hex_keys(70 + gen, 1000 * i, 150))
+        bf = BloomFilter(nb, k)
+        bf.add_many(members)
+        return bf, oracle.build(nb, k, members)
+
+    def check(filters, bitmaps, probes):
+        q = PackedKeys.fixed(probes)
+        want = [np.unpackbits(oracle.probe(bm, k, q), bitorder="little")[:q.n] for bm in bitmaps]
+        keys = _strs(q)
+        for j, key in enumerate(keys):
+            f = j % len(filters)
+            assert filters[f].may_contain(key) == bool(want[f][j]), (f, key)
+        for j, key in enumerate(keys[:60]):
+            base = (7 * j) % (len(filters) - 64)
+            got = may_contain_set(filters[base:base + 64], key)
+            assert got == [bool(want[base + t][j]) for t in range(64)], (base, key)
+
+    pairs = [make(i, 0) for i in range(300)]
+    filters, bitmaps = [p[0] for p in pairs], [p[1] for p in pairs]
+    # probes: members of some filters and keys of none
+    probes = np.concatenate([splitmix_hex_keys(70, 1000 * i, 3) for i in range(0, 300, 2)] +
+                            [splitmix_hex_keys(99, 0, 300)])
+    check(filters, bitmaps, probes)
+    del pairs
+    for i in range(100):  # destroy: the indexes go back to the table
+        filters[i] = None
+    gc.collect()
+    fresh = [make(i, 1) for i in range(100)]
+    for i in range(100):
+        filters[i], bitmaps[i] = fresh[i]
+    del fresh
+    probes = np.concatenate([splitmix_hex_keys(71, 1000 * i, 3) for i in range(100)] +
+                            [splitmix_hex_keys(70, 1000 * i, 2) for i in range(100, 300, 3)] +
+                            [splitmix_hex_keys(98, 0, 300)])
+    check(filters, bitmaps, probes)
+    assert filters[0].last_probe_detail & _native.PBF_DETAIL_RESIDENT

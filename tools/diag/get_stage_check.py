@@ -53,3 +53,36 @@ lib.loop_set.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_char_p, ctyp
 kb = b"".join(enc)
 print("C loop in-process, 16: %.2f us" % lib.loop_set(hs16, 16, kb, 1000, 20000))
 print("C loop in-process, 1:  %.2f us" % lib.loop_set(hs1, 1, kb, 1000, 20000))
+lib.loop_set_gap.restype = ctypes.c_double
+lib.loop_set_gap.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_double]
+for gap in (0.0, 0.5, 1.0, 2.0, 4.0):
+    print("C loop, gap %.1f us: 16 filters %.2f us, 1 filter %.2f us" % (
+        gap, lib.loop_set_gap(hs16, 16, kb, 1000, 20000, gap), lib.loop_set_gap(hs1, 1, kb, 1000, 20000, gap)))
+same16 = (flat[-1]._fast,) * 16
+for _ in range(200):
+    fast.may_contain_set(same16, probes[_])
+t = time.perf_counter()
+for i in range(5000):
+    fast.may_contain_set(same16, probes[i % 1000])
+print("fast.may_contain_set one filter x16: %.2f us" % ((time.perf_counter() - t) / 5000 * 1e6))
+
+
+def dev_stats():
+    r, d = ctypes.c_uint64(), ctypes.c_uint64()
+    L.pbf_resident_stats(0, ctypes.byref(r), ctypes.byref(d))
+    return r.value, d.value
+
+
+for name, fn in (("fast.may_contain_set tuple16", lambda k: fast.may_contain_set(tup16, k)),
+                 ("fast.may_contain 1", lambda k: fast.may_contain(flat[-1]._fast, k))):
+    r0, d0 = dev_stats()
+    t = time.perf_counter()
+    for i in range(5000):
+        fn(probes[i % 1000])
+    dt = (time.perf_counter() - t) / 5000 * 1e6
+    r1, d1 = dev_stats()
+    print("%-30s %.2f us per call, device %.2f us" % (name, dt, (d1 - d0) * 1e-3 / max(1, r1 - r0)))
+r0, d0 = dev_stats()
+print("C loop in-process, 16: %.2f us" % lib.loop_set(hs16, 16, kb, 1000, 20000), end="")
+r1, d1 = dev_stats()
+print(", device %.2f us" % ((d1 - d0) * 1e-3 / max(1, r1 - r0)))

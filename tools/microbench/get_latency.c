@@ -108,13 +108,24 @@ int main(int argc, char** argv) {
             hexkey(start - 500 + (i % 1000), key);
             CK(pbf_may_contain_set(fs + NF - nf, (uint32_t)nf, (const uint8_t*)key, 16, bits));
         }
-        printf("may_contain_set over %2d filters: %.2f us\n", nf, (now_us() - t0) / reps);
+        const double per = (now_us() - t0) / reps;
+        uint64_t r1 = 0, d1 = 0;
+        CK(pbf_resident_stats(0, &r1, &d1));
+        static uint64_t r0 = 0, d0 = 0;
+        printf("may_contain_set over %2d filters: %.2f us (device %.2f us of it)\n", nf, per,
+               r1 > r0 ? (d1 - d0) * 1e-3 / (r1 - r0) : 0.0);
+        r0 = r1;
+        d0 = d1;
     }
     // the same 16 filters, one key repeated (its bitmap lines stay hot)
     hexkey(start - 1, key);
     t0 = now_us();
     for (int i = 0; i < reps; ++i) CK(pbf_may_contain_set(fs, NF, (const uint8_t*)key, 16, bits));
     printf("may_contain_set over 16 filters, one key: %.2f us\n", (now_us() - t0) / reps);
+    uint64_t nreq = 0, dns = 0;
+    CK(pbf_resident_stats(0, &nreq, &dns));
+    printf("resident reader: %llu requests, %.2f us each on the device (seen -> answered)\n",
+           (unsigned long long)nreq, nreq ? dns * 1e-3 / nreq : 0.0);
     for (int f = 0; f < NF; ++f) pbf_destroy(fs[f]);
     return 0;
 }
@@ -128,4 +139,20 @@ double loop_set(pbf_filter_t* const* fs, uint32_t nf, const char* keys16, int nk
     const double t0 = now_us();
     for (int i = 0; i < reps; ++i) pbf_may_contain_set(fs, nf, (const uint8_t*)keys16 + 16 * (i % nkeys), 16, bits);
     return (now_us() - t0) / reps;
+}
+
+// The same loop with a pause of `gap_us` between calls (the caller's own work between gets):
+// microseconds per call, the pause excluded.
+double loop_set_gap(pbf_filter_t* const* fs, uint32_t nf, const char* keys16, int nkeys, int reps, double gap_us) {
+    uint8_t bits[8];
+    double inside = 0;
+    for (int i = 0; i < reps; ++i) {
+        const double g0 = now_us();
+        while (now_us() - g0 < gap_us) {
+        }
+        const double t0 = now_us();
+        pbf_may_contain_set(fs, nf, (const uint8_t*)keys16 + 16 * (i % nkeys), 16, bits);
+        inside += now_us() - t0;
+    }
+    return inside / reps;
 }
