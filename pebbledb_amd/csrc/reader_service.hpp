@@ -28,6 +28,9 @@
 // started is never read from a stale line of this XCD's L2 (the host only posts keys for a filter
 // with no work still queued on its stream).
 #pragma once
+#ifndef PBF_SVC_TICK_AT
+#define PBF_SVC_TICK_AT 0
+#endif
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -179,6 +182,9 @@ __device__ __forceinline__ void svc_answer(SvcBoard* b, uint32_t s, uint32_t req
         L.miss[lane] = 0u;
     }
     __syncthreads();
+#if PBF_SVC_TICK_AT == 1  // (A/B: the wave's time to this point instead of to the answer)
+    const uint64_t t_mark = wall_clock64();
+#endif
     // into the cache: of the lanes whose indexes share an entry, the one whose tag landed writes it
     if (miss) L.ctag[ce] = id;
     __syncthreads();
@@ -191,6 +197,9 @@ __device__ __forceinline__ void svc_answer(SvcBoard* b, uint32_t s, uint32_t req
     h = fmix32(h ^ len);
     if (lane < k) L.hs[lane] = h;
     __syncthreads();
+#if PBF_SVC_TICK_AT == 2
+    const uint64_t t_mark = wall_clock64();
+#endif
     // the AND of bloom_filter.py:71-74 for every filter, without its early exit: pair p = (filter
     // p / k, seed p % k); up to 4 rounds of 64 pairs issue their loads before any is used
     const uint32_t np = nf * k;
@@ -222,9 +231,16 @@ __device__ __forceinline__ void svc_answer(SvcBoard* b, uint32_t s, uint32_t req
             if (!((w[r] >> sh[r]) & 1u)) L.miss[fr[r]] = 1u;
     }
     __syncthreads();
+#if PBF_SVC_TICK_AT == 3
+    const uint64_t t_mark = wall_clock64();
+#endif
     const bool hit = lane < nf && L.miss[lane] == 0u;
     const unsigned long long bal = __ballot(hit);
+#if PBF_SVC_TICK_AT >= 1
+    if (lane == 0) svc_ack(sl, req, uint64_t(bal), uint32_t(t_mark - t_seen));
+#else
     if (lane == 0) svc_ack(sl, req, uint64_t(bal), uint32_t(wall_clock64() - t_seen));
+#endif
     __syncthreads();  // kw, hb, rq and miss are rewritten by the next request
 }
 
