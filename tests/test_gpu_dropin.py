@@ -486,5 +486,13 @@ def test_resident_descriptor_indexes_cached_and_reused(oracle):
     probes = np.concatenate([splitmix_hex_keys(71, 1000 * i, 3) for i in range(100)] +
                             [splitmix_hex_keys(70, 1000 * i, 2) for i in range(100, 300, 3)] +
                             [splitmix_hex_keys(98, 0, 300)])
+    import ctypes
+    r0, d0 = ctypes.c_uint64(), ctypes.c_uint64()
+    _native.check(_native.lib().pbf_resident_stats(filters[0].device, ctypes.byref(r0), ctypes.byref(d0)))
     check(filters, bitmaps, probes)
     assert filters[0].last_probe_detail & _native.PBF_DETAIL_RESIDENT
+    r1, d1 = ctypes.c_uint64(), ctypes.c_uint64()
+    _native.check(_native.lib().pbf_resident_stats(filters[0].device, ctypes.byref(r1), ctypes.byref(d1)))
+    # every probe above was answered by the wave, each in well under a millisecond of its time
+    assert r1.value - r0.value >= probes.shape[0] + 60
+    assert 0 < d1.value - d0.value < (r1.value - r0.value) * 1_000_000
