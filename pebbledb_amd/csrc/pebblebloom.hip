@@ -331,8 +331,8 @@ size_t max_scratch_sets() {
 
 struct alignas(128) pbf_filter {
     // The fields a per-key probe reads (or writes) of every filter it tests, together in the first
-    // 128 bytes: a get over 16 filters from Python otherwise paid ~0.1 us per filter in cache
-    // misses on four lines of each (tools/diag/get_stage_check.py).
+    // 128 bytes (two lines of each filter instead of four; measured neutral for a 16-filter get,
+    // tools/diag/get_stage_check.py, kept as the layout the per-key path reads).
     //
     // Writers (builds, from_bytes, batch probes: anything that touches the handle's state or
     // queues work on its stream) hold mu exclusively; one-key probes of a built filter hold it
