@@ -12,7 +12,9 @@ The bitmap lives in HBM behind a ``pbf_filter_t`` handle (libpebblebloom.so, cty
 serialisation, ``bits``), so an SSTableBuilder-style loop of ``add`` costs one kernel
 pipeline, not one launch per key.  ``may_contain(key)`` — LsmStorage.get's per-key call — is
 answered by the device's resident reader wave (the key posted into mapped pinned memory, no
-launch per key; ``pbf_may_contain``), or one launch where the resident reader does not apply.  Batch
+launch per key; ``pbf_may_contain``, called through the ``_pebblefast`` C extension rather than
+ctypes), or one launch where the resident reader does not apply.  ``lsm_get.candidates_one`` runs
+a whole get's filter stage the same way.  Batch
 entry points ``add_many`` / ``may_contain_many`` take ``list[str]``, ``PackedKeys`` or a
 ``KeyPacker`` directly.
 
