@@ -1,5 +1,11 @@
 """Which path one get's filter stage takes (lsm_get.candidates_one: the C stage or the Python
-loop) and what each costs, on the bench's 16-filter set (bench.py get_set_latency)."""
+loop) and what each costs, on the bench's 16-filter set (bench.py get_set_latency).
+
+Needs tools/microbench/get_latency.so (the same call loop in C, loaded into this process):
+    gcc -O2 -fPIC -shared -DGET_LATENCY_LIB -o tools/microbench/get_latency.so \
+        tools/microbench/get_latency.c -Iinclude -Lpebbledb_amd -lpebblebloom \
+        -Wl,-rpath,'$ORIGIN/../../pebbledb_amd'
+"""
 import sys
 import time
 
