@@ -496,3 +496,18 @@ def test_resident_descriptor_indexes_cached_and_reused(oracle):
     # every probe above was answered by the wave, each in well under a millisecond of its time
     assert r1.value - r0.value >= probes.shape[0] + 60
     assert 0 < d1.value - d0.value < (r1.value - r0.value) * 1_000_000
+
+
+def test_resident_reader_under_filter_churn():
+    """Reader threads run gets over the current filters while a writer keeps replacing them with
+    filters of other sizes (an LSM's flushes and compactions): replaced filters are destroyed when
+    their last reader lets go, their descriptor indexes are reused under a new epoch, and every
+    answer equals the oracle's (tools/diag/reader_churn.py; 20 s runs: ~1M gets, ~40k
+    replacements, no error -- profiles/r06/perkey/s25_churn.log)."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("reader_churn", os.path.join(REPO, "tools", "diag", "reader_churn.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    st = mod.run(seconds=4.0, readers=8)
+    assert not st["errors"], st["errors"][:3]
+    assert st["gets"] > 1000 and st["churn"] > 50, st
