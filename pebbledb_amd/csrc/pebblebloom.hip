@@ -722,10 +722,10 @@ uint64_t groups_cap(bool sort_probe, bool spare) {
     return spare && g >= 256 ? g / 256 * 248 : g;
 }
 
-PartPlan plan_ring(uint32_t B, uint32_t k, uint64_t n, uint32_t kps, bool probe, double share, uint32_t nf = 1,
-                   bool spare = false) {
+PartPlan plan_ring_g(uint32_t B, uint32_t k, uint64_t n, uint32_t kps, bool probe, double share, uint32_t nf,
+                     uint64_t gcap) {
     PartPlan pl{};
-    const uint64_t G0 = std::min<uint64_t>(groups_cap(false, spare), std::max<uint64_t>(1, (n + kps - 1) / kps));
+    const uint64_t G0 = std::min<uint64_t>(gcap, std::max<uint64_t>(1, (n + kps - 1) / kps));
     uint64_t kpw = (n + G0 - 1) / G0;
     kpw = ((kpw + kps - 1) / kps) * kps;
     pl.pg.G = uint32_t(std::max<uint64_t>(1, (n + kpw - 1) / kpw));
@@ -742,6 +742,27 @@ PartPlan plan_ring(uint32_t B, uint32_t k, uint64_t n, uint32_t kps, bool probe,
     pl.pg.spill_cap = uint32_t(std::min<size_t>(4096, (size_t(kRingLdsWords) * 4 - ring_bytes) / spill_entry));
     pl.lds_part = 0;  // k_part_ring declares the CU's whole LDS statically (kRingLdsWords)
     set_gather(pl, B, pl.pg.nq + 1, nf);
+    return pl;
+}
+
+// A multi-filter probe's gather keeps one key bitmap per filter of its partition workgroup's keys
+// in LDS, which caps a pipeline at ~33M keys with one workgroup per CU (C5's 100M keys: 3
+// pipelines, each streaming every filter's bitmap through the set tile test).  So while the
+// gather does not fit, a multi-filter probe plans 2, 3 or 4 rounds of partition workgroups
+// (smaller key bitmaps, one pipeline for the batch); the tile test's per-word table then walks
+// the regions in chunks (PartGeom::tabw).
+PartPlan plan_ring(uint32_t B, uint32_t k, uint64_t n, uint32_t kps, bool probe, double share, uint32_t nf = 1,
+                   bool spare = false) {
+    const uint64_t gcap = groups_cap(false, spare);
+    PartPlan pl = plan_ring_g(B, k, n, kps, probe, share, nf, gcap);
+    static const bool g_forced = std::getenv("PBF_PART_G") != nullptr;  // (A/B: the count as given)
+    if (probe && nf > 1 && !g_forced) {
+        for (uint64_t mult = 2; mult <= 4 && pl.lds_gather > 156 * 1024; ++mult) {
+            const PartPlan p2 = plan_ring_g(B, k, n, kps, probe, share, nf, gcap * mult);
+            if (p2.pg.G <= pl.pg.G) break;  // (too few keys for more workgroups)
+            pl = p2;
+        }
+    }
     return pl;
 }
 
@@ -1005,8 +1026,13 @@ int run_tiled_probe_set(pbf_filter_t* f, pbf_filter_t* const* fs, uint32_t nf, c
     const size_t table_words = size_t(pg.G) * wpr;
     const uint32_t wsh = 32u - uint32_t(__builtin_clz(std::max(wpr, 2u) - 1u));
     const bool tab1_fits = (uint64_t(pg.G - 1) << wsh) < 65536 && uint64_t(pg.G) * B < (uint64_t(1) << 24);
-    const int tab = lds_tile + table_words * 4 <= 160 * 1024 ? 2 : (tab1_fits && lds_tile + table_words * 2 <= 160 * 1024 ? 1 : 0);
-    lds_tile += tab == 2 ? table_words * 4 : (tab == 1 ? table_words * 2 : 0);
+    // TAB 1 in chunks of whole regions when the whole table does not fit beside the tile (at
+    // least one region's words per chunk)
+    const size_t tab1_room = lds_tile < 160 * 1024 ? (160 * 1024 - lds_tile) / 2 & ~size_t(1) : 0;
+    const int tab = lds_tile + table_words * 4 <= 160 * 1024 ? 2 : (tab1_fits && tab1_room >= wpr ? 1 : 0);
+    PartGeom tpg = pg;  // (the tile test's copy: tabw)
+    tpg.tabw = tab == 1 && table_words > tab1_room ? uint32_t(tab1_room) : 0u;
+    lds_tile += tab == 2 ? table_words * 4 : (tab == 1 ? (tpg.tabw ? size_t(tpg.tabw) : table_words) * 2 : 0);
     // a region word's global index (region * cap/32 + word) is 32-bit
     if (uint64_t(pg.G) * B * (pg.cap / 32) >= (uint64_t(1) << 32)) return fail(PBF_ERR_INVALID, "probe scratch too large");
     auto tprobe = tab == 2 ? k_tile_probe<2> : (tab == 1 ? k_tile_probe<1> : k_tile_probe<0>);
@@ -1045,11 +1071,11 @@ int run_tiled_probe_set(pbf_filter_t* f, pbf_filter_t* const* fs, uint32_t nf, c
     // every filter's tile test (one XCD-aware launch for a set), then ONE gather over the shared
     // region entries
     if (nf == 1) {
-        tprobe<<<B, 1024, lds_tile, s>>>(tm, pg, regions, fill, fs[0]->bitmap, R);
+        tprobe<<<B, 1024, lds_tile, s>>>(tm, tpg, regions, fill, fs[0]->bitmap, R);
     } else {
         HIP_TRY(allow_lds(tprobe_set, lds_tile));
         const uint32_t tgrid = ((B + 7) / 8) * 8 * nf;
-        tprobe_set<<<tgrid, 1024, lds_tile, s>>>(tm, pg, regions, fill, ps, R, r_words);
+        tprobe_set<<<tgrid, 1024, lds_tile, s>>>(tm, tpg, regions, fill, ps, R, r_words);
     }
     LAUNCHED(f, nf == 1 ? "k_tile_probe" : "k_tile_probe_set");
     // the set gather: 1024 threads when its LDS admits one workgroup per CU (C5's 8 key bitmaps)

@@ -132,6 +132,7 @@ struct PartGeom {
     uint32_t ring;     // ring partition: LDS ring entries per tile (0 = counting-sort partition)
     uint32_t spill_cap;  // ring partition: entries of the LDS spill buffer
     uint32_t scap;       // counting-sort partition: stage entries (a sub-chunk is placed in windows of scap)
+    uint32_t tabw;       // tile test, TAB 1: words of the per-word table (0 = all of a tile's words)
 };
 
 constexpr uint32_t kSlotShift = 20;   // probe entry = key-in-group << 20 | position in tile
@@ -759,54 +760,71 @@ __device__ __forceinline__ void tile_probe_body(uint32_t* smem, uint32_t b, cons
     }
     lds_barrier();
     block_exclusive_scan(fills, wpre, G, ws);
-    if constexpr (TAB > 0) {
-        for (uint32_t q = tid; q < G; q += nt) {
-            const uint32_t base = uint32_t(region_id(q, b, G, B)) * wpr;
-            for (uint32_t c = wpre[q]; c < wpre[q + 1]; ++c) {
-                if constexpr (TAB == 2)
-                    wo[c] = base + (c - wpre[q]);
-                else
-                    wq[c] = uint16_t((q << wsh) | (c - wpre[q]));
-            }
-        }
-    }
-    if (dma) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's tile pieces landed
-    lds_barrier();
-    const uint32_t total = wpre[G];
     const uint32_t lane = tid & 63, wave = tid >> 6, nwaves = nt >> 6;
     const uint32_t l = lane & 7, wsub = lane >> 3;  // piece of the word, word of the instruction
     const uint32_t stride = nwaves * 8;
-    for (uint32_t c0 = wave * 8; c0 < total; c0 += stride * U) {
-        uint4 v[U];
-        uint32_t oo[U];
+    // an entry's tile word: one bit-field extract of bits [5, tb); its bit: one more (the
+    // hardware takes the offset's low 5 bits, so no mask)
+    const uint32_t wbits = tm.tb - 5;
+    auto bit = [&](uint32_t x) { return __builtin_amdgcn_ubfe(tile[__builtin_amdgcn_ubfe(x, 5u, wbits)], x, 1u); };
+    // the words [c_lo, c_hi) of the tile's regions; TAB 1's table holds word c at c - c_lo
+    auto stream = [&](uint32_t c_lo, uint32_t c_hi) {
+        for (uint32_t c0 = c_lo + wave * 8; c0 < c_hi; c0 += stride * U) {
+            uint4 v[U];
+            uint32_t oo[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint32_t cc = min(c0 + u * stride + wsub, total - 1);  // unconditional loads
-            if constexpr (TAB == 2) {
-                oo[u] = wo[cc];
-            } else if constexpr (TAB == 1) {
-                const uint32_t e = wq[cc];
-                oo[u] = __umul24(__umul24(e >> wsh, B) + b, wpr) + (e & ((1u << wsh) - 1u));
-            } else {
-                const uint32_t qq = bucket_of(wpre, G, cc);
-                oo[u] = uint32_t(region_id(qq, b, G, B)) * wpr + (cc - wpre[qq]);
+            for (int u = 0; u < U; ++u) {
+                const uint32_t cc = min(c0 + u * stride + wsub, c_hi - 1);  // unconditional loads
+                if constexpr (TAB == 2) {
+                    oo[u] = wo[cc];
+                } else if constexpr (TAB == 1) {
+                    const uint32_t e = wq[cc - c_lo];
+                    oo[u] = __umul24(__umul24(e >> wsh, B) + b, wpr) + (e & ((1u << wsh) - 1u));
+                } else {
+                    const uint32_t qq = bucket_of(wpre, G, cc);
+                    oo[u] = uint32_t(region_id(qq, b, G, B)) * wpr + (cc - wpre[qq]);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) v[u] = ld_stream_nt<NT>(regions + uint64_t(oo[u]) * 32 + l * 4);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                uint32_t r = (bit(v[u].x) | (bit(v[u].y) << 8) | (bit(v[u].z) << 16) | (bit(v[u].w) << 24)) << l;
+                // OR over the word's 8 lanes: swap neighbours, pairs, then the two quads
+                r |= uint32_t(__builtin_amdgcn_mov_dpp(int(r), 0xB1, 0xF, 0xF, false));   // quad_perm [1,0,3,2]
+                r |= uint32_t(__builtin_amdgcn_mov_dpp(int(r), 0x4E, 0xF, 0xF, false));   // quad_perm [2,3,0,1]
+                r |= uint32_t(__builtin_amdgcn_mov_dpp(int(r), 0x141, 0xF, 0xF, false));  // row_half_mirror
+                if (l == 0 && c0 + u * stride + wsub < c_hi) R[oo[u]] = r;
             }
         }
-#pragma unroll
-        for (int u = 0; u < U; ++u) v[u] = ld_stream_nt<NT>(regions + uint64_t(oo[u]) * 32 + l * 4);
-        // an entry's tile word: one bit-field extract of bits [5, tb); its bit: one more (the
-        // hardware takes the offset's low 5 bits, so no mask)
-        const uint32_t wbits = tm.tb - 5;
-        auto bit = [&](uint32_t x) { return __builtin_amdgcn_ubfe(tile[__builtin_amdgcn_ubfe(x, 5u, wbits)], x, 1u); };
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            uint32_t r = (bit(v[u].x) | (bit(v[u].y) << 8) | (bit(v[u].z) << 16) | (bit(v[u].w) << 24)) << l;
-            // OR over the word's 8 lanes: swap neighbours, pairs, then the two quads
-            r |= uint32_t(__builtin_amdgcn_mov_dpp(int(r), 0xB1, 0xF, 0xF, false));   // quad_perm [1,0,3,2]
-            r |= uint32_t(__builtin_amdgcn_mov_dpp(int(r), 0x4E, 0xF, 0xF, false));   // quad_perm [2,3,0,1]
-            r |= uint32_t(__builtin_amdgcn_mov_dpp(int(r), 0x141, 0xF, 0xF, false));  // row_half_mirror
-            if (l == 0 && c0 + u * stride + wsub < total) R[oo[u]] = r;
+    };
+    if constexpr (TAB == 1) {
+        // the table takes the regions in chunks whose words fit it (pg.tabw words; every region's
+        // <= wpr words fit): a batch with more regions per tile than the LDS holds a table for
+        // (more partition workgroups, e.g. C5's 100M keys in one pipeline) still reads one LDS
+        // word per region word, at one more barrier pair per chunk
+        const uint32_t tabw = pg.tabw ? pg.tabw : 0xFFFFFFFFu;
+        for (uint32_t q0 = 0; q0 < G;) {
+            const uint32_t c_lo = wpre[q0];
+            const uint32_t q1 = tabw >= wpre[G] - c_lo ? G : max(q0 + 1, bucket_of(wpre, G + 1, c_lo + tabw));
+            for (uint32_t q = q0 + tid; q < q1; q += nt)
+                for (uint32_t c = wpre[q]; c < wpre[q + 1]; ++c) wq[c - c_lo] = uint16_t((q << wsh) | (c - wpre[q]));
+            if (q0 == 0 && dma) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's tile pieces landed
+            lds_barrier();
+            stream(c_lo, wpre[q1]);
+            q0 = q1;
+            if (q0 < G) lds_barrier();  // every wave is done with this chunk's table
         }
+    } else {
+        if constexpr (TAB == 2) {
+            for (uint32_t q = tid; q < G; q += nt) {
+                const uint32_t base = uint32_t(region_id(q, b, G, B)) * wpr;
+                for (uint32_t c = wpre[q]; c < wpre[q + 1]; ++c) wo[c] = base + (c - wpre[q]);
+            }
+        }
+        if (dma) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's tile pieces landed
+        lds_barrier();
+        stream(0, wpre[G]);
     }
 }
 
