@@ -61,7 +61,7 @@ for step in "$@"; do
     traffic) traffic c2 --steps 5 --warmup 2 ;;
     traffic_c3) TRAFFIC_ARGS="--probe-scale 2.0" traffic c3 --config c3 --steps 2 --warmup 1 ;;  # two equal 100M-key pipelines per probe pass
     traffic_c4) traffic c4 --config c4 --steps 2 --warmup 1 ;;  # per-filter build pass (bench scales by the rank's filters)
-    traffic_c5) TRAFFIC_ARGS="--probe-scale 3.0" traffic c5 --config c5 --steps 2 --warmup 1 --no-host-c5 --no-compare ;;  # three equal pipelines
+    traffic_c5) TRAFFIC_ARGS="--probe-scale 1.0" traffic c5 --config c5 --steps 2 --warmup 1 --no-host-c5 --no-compare ;;  # one pipeline (the 100M-key batch)
     pmcall) run pmcall 2400 tools/pmc_passes.sh gpurun_out/pmcall ;;
     pmc_c3) run pmc_c3 2400 tools/pmc_passes.sh gpurun_out/pmc_c3 --config c3 ;;
     pmc_c4) run pmc_c4 2400 tools/pmc_passes.sh gpurun_out/pmc_c4 --config c4 ;;
